@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Benchmark: λ-bin·layer flux updates/s at 60 layers × 500k λ (BASELINE.json metric).
+
+Workload: hot Jupiter, 60 layers × 500,000 wavelengths, 8 opacity
+species (H2O, CO, CO2, CH4, Na, K + H2-H2/H2-He CIA), 16 T-nodes, synthetic separable
+tables generated on the device.  One step = one radiative-equilibrium T–P iteration
+(emit sweep + absorb sweep, each with its bolometric reduction, dT update and the
+convergence test) = 2 × 59 × 500k flux updates, always fully computed (convergence is
+tracked but does not stop the timed work).  With --gpus N the 500k wavelengths are
+sharded over N ranks (strong scaling) with one RCCL all-gather per sweep.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n-lam", type=int, default=500_000)
+    ap.add_argument("--n-layers", type=int, default=60)
+    ap.add_argument("--n-T", type=int, default=16)
+    ap.add_argument("--rad-eq-max", type=int, default=200,
+                    help="max T-P iterations for the iterations-to-radiative-equilibrium run")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-lam", type=int, default=50_000)
+    return ap.parse_args()
+
+
+class Dist:
+    """torch.distributed (gloo, CPU only) for rendezvous, barriers and timing reductions;
+    the data-path collective is RCCL inside the native engine."""
+
+    def __init__(self, n):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != n:
+            raise SystemExit(f"--gpus {n} but WORLD_SIZE={self.world}")
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast_bytes(self, b):
+        if not self.dist:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+
+def cpu_baseline(w, n_sample, steps=1):
+    """Oracle (NumPy restatement of the reference path, 1 core) on a wavelength sample of the
+    same workload: `steps` T-P iterations, timed with perf_counter."""
+    from oracle import frei_oracle as O
+    lam = w["lam"]
+    idx = np.linspace(0, lam.size - 1, n_sample).round().astype(int)
+    tabs = {n: O.Table(O.SeparableValues(w["base"][s][idx], w["fp"][s], w["fT"][s]), w["p"],
+                       w["T_nodes"]) for s, n in enumerate(w["names"])}
+    lam_s = lam[idx]
+    Ft = O.F_TOA(lam_s)
+    t0 = time.perf_counter()
+    O.emission_spectrum(tabs, w["T0"], w["p"], lam_s, Ft, 2478.6519476149147,
+                        4.0142926168559996e-24, 1, n_timesteps=steps,
+                        n_zero_crossings=10 ** 9, convergence_dT=-1.0, mmr=w["mmr"])
+    dt = time.perf_counter() - t0
+    updates = (2 * steps + 1) * (w["p"].size - 1) * n_sample   # incl. the final emit
+    return updates / dt, dt
+
+
+def main():
+    a = parse()
+    d = Dist(a.gpus)
+    from frei_amd import _native as N
+    from frei_amd.engine import Engine, partition
+    from frei_amd.opacity import SeparableTable
+    from frei_amd.workloads import bytes_per_update, c3
+
+    w = c3(n_layers=a.n_layers, n_lam=a.n_lam, n_T=a.n_T)
+    nL, n_lam, S = a.n_layers, a.n_lam, len(w["names"])
+    lo, hi = partition(n_lam, d.world, d.rank)
+    comm = None
+    if d.world > 1:
+        uid = None
+        if d.rank == 0:
+            import ctypes
+            buf = ctypes.create_string_buffer(128)
+            N.check(N.lib().frei_comm_unique_id(buf))
+            uid = buf.raw
+        uid = d.bcast_bytes(uid)
+        comm = (d.world, d.rank, uid)
+    tabs = {n: SeparableTable(w["base"][s], w["fp"][s], w["fT"][s], w["p"], w["T_nodes"])
+            for s, n in enumerate(w["names"])}
+    eng = Engine(w["lam"], w["p"], tabs, mmr=w["mmr"], device=d.local, lam_slice=(lo, hi),
+                 comm=comm)
+
+    # ---- timed fixed-work T-P iterations
+    eng.state_init(w["T0"])
+    eng.iterate(a.warmup)
+    eng.synchronize()
+    d.barrier()
+    t0 = time.perf_counter()
+    eng.timing(True)
+    eng.iterate(a.steps)
+    eng.synchronize()
+    t1 = time.perf_counter()
+    d.barrier()
+    sweep_ms, n_sweeps = eng.timing_read()
+    eng.timing(False)
+    elapsed = d.max(t1 - t0)
+    updates_per_step = 2 * (nL - 1) * n_lam
+    value = updates_per_step * a.steps / elapsed
+    ms_per_step = elapsed / a.steps * 1e3
+
+    # ---- roofline of the dominant kernel (sweep), per launch, this rank's slice
+    bpu = bytes_per_update(S)
+    avg_sweep_s = (sweep_ms / max(n_sweeps, 1)) * 1e-3
+    bytes_launch = bpu * (nL - 1) * (hi - lo)
+    achieved = bytes_launch / avg_sweep_s
+    achieved = d.max(achieved) if d.world > 1 else achieved
+
+    # ---- iterations to radiative equilibrium (reference convergence test)
+    t2 = time.perf_counter()
+    out = eng.run(w["T0"], n_timesteps=a.rad_eq_max, n_zero_crossings=2, convergence_dT=3.0,
+                  alpha=1.0, want_dtaus=False)
+    t3 = time.perf_counter()
+    rad_eq_wall = d.max(t3 - t2)
+    n_iter = out["n_iter"]
+
+    cpu = None
+    if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
+        rate, dt = cpu_baseline(w, min(a.cpu_lam, n_lam))
+        cpu = {"value": rate, "unit": "updates/s", "cores": 1, "kind": "port",
+               "sample": f"oracle (NumPy restatement of frei's path), {nL} layers x "
+                         f"{min(a.cpu_lam, n_lam)} lambda (evenly strided sample of the same "
+                         f"grid), {S} species, 1 T-P iteration + final emit, {dt:.1f} s"}
+    eng.close()
+    if d.rank == 0:
+        line = {
+            "metric": "lambda-bin*layer flux updates/sec at 60 layers x 500k lambda",
+            "value": value,
+            "unit": "updates/s",
+            "n_gpus": d.world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (separable line-forest opacity tables generated on device)",
+            "config": {"workload": f"C3/C4: {nL} layers x {n_lam} lambda, {S} species "
+                                   f"(H2O/CO/CO2/CH4/Na/K + H2-H2/H2-He CIA), {a.n_T} T-nodes, "
+                                   "1 step = 1 T-P iteration (emit+absorb)",
+                       "n_layers": nL, "n_lambda": n_lam, "n_species": S, "n_T": a.n_T,
+                       "parallelism": f"lambda-shard x{d.world} (RCCL all-gather per sweep)"},
+            "tp_iters_per_s": 1e3 / ms_per_step,
+            "rad_eq": {"iterations": n_iter, "max_iterations": a.rad_eq_max,
+                       "wall_s": rad_eq_wall, "iters_per_s": n_iter / rad_eq_wall},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM, "traffic": None,
+                         "kernel": "sweep_kernel", "bytes_per_update": bpu,
+                         "avg_launch_ms": avg_sweep_s * 1e3, "launches": n_sweeps},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

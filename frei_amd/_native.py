@@ -1,0 +1,97 @@
+"""ctypes binding of the C ABI in include/frei_hip.h (libfrei_hip.so, built in-tree).
+
+There is no CPU fallback: if the shared library is missing or fails to load, every
+compute entry point raises ``RuntimeError`` (build it with ``python -m frei_amd.build``
+or ``__graft_entry__.build()``).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfrei_hip.so")
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+
+# name -> (restype, argtypes); mirrors include/frei_hip.h exactly
+SIGNATURES = {
+    "frei_version": (ctypes.c_int, []),
+    "frei_last_error": (ctypes.c_char_p, []),
+    "frei_device_count": (ctypes.c_int, [_ip]),
+    "frei_ctx_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int, _i64,
+                                       ctypes.c_int]),
+    "frei_ctx_destroy": (ctypes.c_int, [_vp]),
+    "frei_set_grid": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, ctypes.c_double,
+                                     ctypes.c_double]),
+    "frei_set_table": (ctypes.c_int, [_vp, ctypes.c_int, _dp, _dp, ctypes.c_int, _dp,
+                                      ctypes.c_int]),
+    "frei_set_table_separable": (ctypes.c_int, [_vp, ctypes.c_int, _dp, _dp, _dp,
+                                                ctypes.c_double, ctypes.c_double, _dp,
+                                                ctypes.c_int, _dp, ctypes.c_int]),
+    "frei_set_mmr": (ctypes.c_int, [_vp, _dp]),
+    "frei_set_fluxes": (ctypes.c_int, [_vp, _dp, _dp]),
+    "frei_get_fluxes": (ctypes.c_int, [_vp, _dp, _dp]),
+    "frei_set_temperatures": (ctypes.c_int, [_vp, _dp]),
+    "frei_get_temperatures": (ctypes.c_int, [_vp, _dp]),
+    "frei_sweep": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double, _dp, _dp, _dp]),
+    "frei_run": (ctypes.c_int, [_vp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                ctypes.c_double, _ip, _dp, _dp, _dp, _dp]),
+    "frei_state_init": (ctypes.c_int, [_vp, _dp]),
+    "frei_iterate": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                    ctypes.c_double]),
+    "frei_synchronize": (ctypes.c_int, [_vp]),
+    "frei_kappa": (ctypes.c_int, [_vp, ctypes.c_double, ctypes.c_double, _dp, _dp]),
+    "frei_propagate_fluxes": (ctypes.c_int, [ctypes.c_int, _i64, _dp, _dp, _dp, _dp,
+                                             ctypes.c_double, ctypes.c_double, _dp, _dp, _dp,
+                                             _dp]),
+    "frei_comm_unique_id": (ctypes.c_int, [_vp]),
+    "frei_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp]),
+    "frei_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "frei_timing_read": (ctypes.c_int, [_vp, _dp, _ip]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libfrei_hip.so (raises RuntimeError if it is absent: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"frei_amd: native library {LIB_PATH} is missing; build it with "
+                               "`python -m frei_amd.build` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().frei_last_error().decode(errors="replace")
+        raise RuntimeError(f"frei_hip: {msg}")
+
+
+def dptr(a):
+    """Pointer to a C-contiguous float64 array (or NULL for None)."""
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"], "need C-contiguous float64"
+    return a.ctypes.data_as(_dp)
+
+
+def f64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib().frei_device_count(ctypes.byref(n)))
+    return n.value

@@ -1,0 +1,185 @@
+// frei_device.h — shared host/device definitions of the frei MI355X engine.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+namespace frei {
+
+// CODATA 2018 (astropy 4.3.1, the reference's unit backend), cgs.
+constexpr double kH = 6.62607015e-27;
+constexpr double kC = 29979245800.0;
+constexpr double kHC = kH * kC;                       // h*c, as the reference forms it
+constexpr double kKB = 1.380649e-16;
+constexpr double kMP = 1.67262192369e-24;
+constexpr double kMbarDefault = 2.4 * kMP;            // twostream.py:23 default m_bar
+constexpr double kSigmaSB = 5.6703744191844314e-05;   // astropy sigma_sb in cgs
+constexpr double kPi = 3.141592653589793;
+
+constexpr int kEmit = 0;
+constexpr int kAbsorb = 1;
+constexpr int kBlock = 256;  // 4 wave64 per workgroup
+constexpr int kMaxLayers = 1024;
+
+// Sweep step k -> layer index (emit: twostream.py:356, absorb: :491).
+__host__ __device__ inline int step_layer(int dir, int k, int nL) {
+  return dir == kEmit ? k + 1 : nL - 2 - k;
+}
+
+// Per sweep step, wave-uniform.
+struct StepP {
+  double T1, T2;  // K
+  double dm;      // (p1 - p2) / g, g cm^-2 (twostream.py:227-231)
+  int32_t layer;  // i
+  int32_t top;    // emit top layer: F_2_down = F_TOA, F_2_up not stored (Q3)
+  int64_t pad;
+};
+
+// Interpolation term of one species at one layer (opacity.py:250-263).
+struct TermP {
+  const double* row[4];  // table rows (device pointers), corner order of scipy interpn
+  double w[4];           // weights (1 * w_p) * w_T
+  double mmr;            // mass mixing ratio
+  double x1, dx;         // single-T mode: p - p_lo, p_hi - p_lo (scipy interp1d)
+  int32_t nrow;          // rows used (0 = outside the hull); -1 = single-T mode
+  int32_t pad;
+};
+
+// Per species metadata.
+struct SpecMeta {
+  const double* tab;  // [n_p][n_T][n_lam] device
+  int64_t n_lam;
+  int32_t n_p, n_T;
+  int32_t t_off;      // offset of this species' sorted T nodes in tnodes/tperm
+  int32_t one_T;      // single unique temperature -> pressure-only interpolation
+};
+
+// Pressure bracket of one species at one layer (T independent, computed at load time).
+struct PMeta {
+  int32_t p_lo, p_hi;    // table pressure rows (memory index) of the bracket
+  double wp_lo, wp_hi;   // scipy weights (1 - y, y)
+  double x1, dx;         // interp1d form for single-T tables
+  int32_t oob;           // outside the pressure hull -> fill 0
+  int32_t pad;
+};
+
+// scipy RegularGridInterpolator._find_indices on an ascending grid (searchsorted left).
+__host__ __device__ inline void bracket(const double* g, int n, double x, int& i, double& y,
+                                        int& oob) {
+  int lo = 0, hi = n;  // number of nodes < x
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (g[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  i = lo - 1;
+  if (i < 0) i = 0;
+  if (i > n - 2) i = n - 2;
+  y = (x - g[i]) / (g[i + 1] - g[i]);
+  oob = (x < g[0] || x > g[n - 1]) ? 1 : 0;
+}
+
+// Build the interpolation term at temperature T.  With `fast`, the result always has
+// two rows (the T bracket in the on-node pressure slab), OOB encoded as zero weights.
+__host__ __device__ inline TermP make_term(const SpecMeta& sm, const PMeta& pm,
+                                           const double* tnodes, const int32_t* tperm,
+                                           double mmr, double T, int fast) {
+  TermP t;
+  for (int r = 0; r < 4; ++r) { t.row[r] = sm.tab; t.w[r] = 0.0; }
+  t.mmr = mmr;
+  t.x1 = 0.0;
+  t.dx = 1.0;
+  t.nrow = 0;
+  t.pad = 0;
+  const int64_t rowlen = sm.n_lam;
+  if (sm.one_T) {
+    if (pm.oob) return t;
+    const int tp = tperm[sm.t_off];
+    t.row[0] = sm.tab + ((int64_t)pm.p_lo * sm.n_T + tp) * rowlen;
+    t.row[1] = sm.tab + ((int64_t)pm.p_hi * sm.n_T + tp) * rowlen;
+    t.x1 = pm.x1;
+    t.dx = pm.dx;
+    t.nrow = -1;
+    return t;
+  }
+  int it, oobT;
+  double yt;
+  bracket(tnodes + sm.t_off, sm.n_T, T, it, yt, oobT);
+  if (pm.oob || oobT) {
+    if (fast) t.nrow = 2;  // zero weights on valid rows
+    return t;
+  }
+  const int tlo = tperm[sm.t_off + it], thi = tperm[sm.t_off + it + 1];
+  const int pr[2] = {pm.p_lo, pm.p_hi};
+  const double wp[2] = {pm.wp_lo, pm.wp_hi};
+  const int tr[2] = {tlo, thi};
+  const double wt[2] = {1.0 - yt, yt};
+  int n = 0;
+  for (int a = 0; a < 2; ++a) {
+    if (wp[a] == 0.0) continue;  // on-node pressure: the other slab has weight 0
+    for (int b = 0; b < 2; ++b) {
+      t.row[n] = sm.tab + ((int64_t)pr[a] * sm.n_T + tr[b]) * rowlen;
+      t.w[n] = (1.0 * wp[a]) * wt[b];
+      ++n;
+    }
+  }
+  t.nrow = n;
+  return t;
+}
+
+struct SetupArgs {
+  int n_layers, n_species, fast;
+  double* T;               // device temperatures [n_layers]
+  const double* p;         // device pressures (dyn cm^-2)
+  double p_top2, g;
+  const SpecMeta* spec;
+  const PMeta* pmeta;      // [n_species][n_layers]
+  const double* tnodes;
+  const int32_t* tperm;
+  const double* mmr;       // [n_species][n_layers]
+  StepP* steps;            // [n_layers - 1]
+  TermP* terms;            // [n_layers - 1][n_species]
+};
+
+struct SweepArgs {
+  int64_t n_lam;
+  int n_steps, n_species, force;
+  const double *c1, *lk, *sig, *wtr, *ftoa;
+  const StepP* steps;
+  const TermP* terms;
+  double* F_up;
+  double* F_down;
+  double* dtaus;           // optional [n_layers][n_lam]
+  double* part;            // [n_steps*4][nblocks]
+  const int* conv;
+};
+
+struct UpdateArgs {
+  SetupArgs su;
+  int dir, next_dir, nranks, force, track, stop_on_conv, n_zero_crossings, hist_cap;
+  double m_bar, alpha, convergence_dT;
+  const double* Fb;        // [nranks][n_steps*4]
+  double* dT_out;          // [n_layers] optional
+  double* bol_out;         // [n_layers][4] optional
+  double *Tb, *Ta, *hist;
+  int32_t *flips, *prev_sign, *ndiff;
+  int* iter;
+  int* conv;
+};
+
+// launchers (frei_kernels.hip)
+void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st);
+void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
+                   int force, hipStream_t st);
+void launch_setup(const SetupArgs& u, int dir, hipStream_t st);
+void launch_update(const UpdateArgs& a, hipStream_t st);
+void launch_propagate(int64_t n, const double* c1, const double* lk, const double* F1u,
+                      const double* F2d, double T1, double T2, const double* dtau,
+                      const double* w0, double* F2u, double* F1d, hipStream_t st);
+void launch_kappa(int64_t n, const TermP* terms, int nS, const double* sig, double* k,
+                  hipStream_t st);
+void launch_gen_table(double* tab, const double* base, const double* fp, const double* fT,
+                      int n_p, int n_T, int64_t n_lam, double lo, double hi, hipStream_t st);
+void launch_fill(double* x, int64_t n, double v, hipStream_t st);
+
+}  // namespace frei

@@ -1,0 +1,433 @@
+// frei_kernels.hip — gfx950 (CDNA4) kernels of the two-stream radiative-transfer engine.
+//
+// Hot path of bmorris3/frei:
+//   K1 sweep_kernel   one lane per wavelength bin, loop over layers inside the lane
+//                     (emit: twostream.py:351-407, absorb: 486-536) with the species-summed
+//                     opacity assembly fused in (K2, opacity.py:203-269), Planck reuse
+//                     between adjacent layers, in-place flux update and the per-layer
+//                     bolometric trapezoid partials (twostream.py:16-20, 396-398) reduced
+//                     wave -> block in a fixed order.
+//   reduce_kernel     deterministic sum of the per-block partials -> [steps][4].
+//   update_kernel     K4/K5: per-layer scalar physics (twostream.py:23-43, 180-287) -> dT,
+//                     T <- T - dT (Q11), absorb temperature history and the reference's
+//                     convergence test (core.py:301-318), then the next sweep's
+//                     per-layer interpolation terms (setup) — the T-P loop never leaves
+//                     the device.
+//
+// Numerics: fp64 throughout, compiled with -ffp-contract=off and the reference's
+// expression order, so results differ from NumPy only by the last-ulp differences of
+// exp/expm1/sqrt (ocml vs libm).  See DESIGN.md "Parity".
+#include "frei_device.h"
+
+namespace frei {
+
+// ---------------------------------------------------------------- device math
+__device__ __forceinline__ double planck(double c1, double lk, double T) {
+  // twostream.py:64-67: 2hc^2/lam^5 / expm1(hc / (lam k T))
+  return c1 / expm1(kHC / (lk * T));
+}
+
+// twostream.py:97-177 with g_0 = 0 (call sites 389, 518), E() of :70-94.
+__device__ __forceinline__ void two_stream(double w0, double dtau, double B1, double B2,
+                                           double F1u, double F2d, double& F2u,
+                                           double& F1d) {
+  const double E = (w0 > 0.1) ? ((1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0)) : 1.0;
+  const double Emw = E - w0;
+  const double Tr = exp((-2.0 * sqrt(E * Emw)) * dtau);
+  const double r = sqrt(Emw / E);
+  const double zp = 0.5 * (1.0 + r);
+  const double zm = 0.5 * (1.0 - r);
+  const double Tr2 = Tr * Tr;
+  const double zm2 = zm * zm;
+  const double zp2 = zp * zp;
+  const double chi = zm2 * Tr2 - zp2;
+  const double xi = (zp * zm) * (1.0 - Tr2);
+  const double psi = (zm2 - zp2) * Tr;
+  const double pi_w = (kPi * (1.0 - w0)) / Emw;
+  const double q = ((B1 - B2) / dtau) / (2.0 * E);
+  const double ic = 1.0 / chi;
+  F2u = ic * ((psi * F1u - xi * F2d) +
+              pi_w * ((B2 * (chi + xi) - psi * B1) + q * ((chi - psi) - xi)));
+  F1d = ic * ((psi * F2d - xi * F1u) +
+              pi_w * ((B1 * (chi + xi) - psi * B2) + q * ((xi + psi) - chi)));
+}
+
+// Species-summed opacity at one wavelength (opacity.py:250-269).  FAST: every term is
+// exactly two T-bracket rows of the layer's own pressure slab (pressure on a node).
+template <int S, bool FAST>
+__device__ __forceinline__ double kappa_at(const TermP* __restrict__ t, int nS, int64_t j,
+                                           double sig) {
+  double tot = 0.0;
+  if constexpr (FAST) {
+    double v[2 * S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {  // issue every table load before the first use
+      v[2 * s] = __builtin_nontemporal_load(t[s].row[0] + j);
+      v[2 * s + 1] = __builtin_nontemporal_load(t[s].row[1] + j);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double acc = (0.0 + v[2 * s] * t[s].w[0]) + v[2 * s + 1] * t[s].w[1];
+      double ops = t[s].mmr * acc;
+      if (S > 1) ops = isnan(ops) ? 0.0 : ops;  // xarray nansum for S > 1 (Q8)
+      tot = (s == 0) ? ops : tot + ops;
+    }
+  } else {
+    for (int s = 0; s < nS; ++s) {
+      double acc;
+      if (t[s].nrow < 0) {  // single-T table: scipy interp1d over pressure
+        const double lo = t[s].row[0][j], hi = t[s].row[1][j];
+        acc = ((hi - lo) / t[s].dx) * t[s].x1 + lo;
+      } else {
+        acc = 0.0;
+        for (int r = 0; r < t[s].nrow; ++r) acc = acc + t[s].row[r][j] * t[s].w[r];
+      }
+      double ops = t[s].mmr * acc;
+      if (nS > 1) ops = isnan(ops) ? 0.0 : ops;
+      tot = (s == 0) ? ops : tot + ops;
+    }
+  }
+  return tot + sig;  // k includes sigma (Q1)
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------- K1: sweep
+template <int DIR, int S, bool FAST>
+__global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
+  if (!a.force && *a.conv) return;
+  extern __shared__ double red[];  // [wave][step][4]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int64_t nl = a.n_lam;
+  const int64_t j0 = (int64_t)blockIdx.x * kBlock + tid;
+  const bool act = j0 < nl;
+  const int64_t j = act ? j0 : nl - 1;
+  const double c1 = a.c1[j], lk = a.lk[j], sig = a.sig[j];
+  const double wt = act ? a.wtr[j] : 0.0;
+  double* __restrict__ Fu = a.F_up;
+  double* __restrict__ Fd = a.F_down;
+  const int nS = a.n_species;
+  const int ns = a.n_steps;
+
+  double carry, Bc;
+  {
+    const StepP s0 = a.steps[0];
+    if (DIR == kEmit) {  // fresh F_up carried upward (twostream.py:383)
+      carry = Fu[(int64_t)s0.layer * nl + j];
+      Bc = planck(c1, lk, s0.T1);
+    } else {             // fresh F_down carried downward (twostream.py:511)
+      carry = Fd[(int64_t)(s0.layer + 1) * nl + j];
+      Bc = planck(c1, lk, s0.T2);
+    }
+  }
+  for (int k = 0; k < ns; ++k) {
+    const StepP sp = a.steps[k];
+    const int i = sp.layer;
+    const double kap = kappa_at<S, FAST>(a.terms + (int64_t)k * nS, nS, j, sig);
+    const double dtau = sp.dm * kap;             // twostream.py:227-231
+    const double w0 = sig / (sig + kap);         // twostream.py:376-378
+    double B1, B2, F1u, F2d;
+    if (DIR == kEmit) {
+      B1 = Bc;
+      B2 = sp.top ? Bc : planck(c1, lk, sp.T2);
+      F1u = carry;
+      F2d = sp.top ? a.ftoa[j] : Fd[(int64_t)(i + 1) * nl + j];  // stale (Q2, Q3)
+    } else {
+      B2 = Bc;
+      B1 = planck(c1, lk, sp.T1);
+      F2d = carry;
+      F1u = Fu[(int64_t)i * nl + j];                               // stale (Q2)
+    }
+    double F2u, F1d;
+    two_stream(w0, dtau, B1, B2, F1u, F2d, F2u, F1d);
+    if (act) {
+      if (DIR == kAbsorb || !sp.top) Fu[(int64_t)(i + 1) * nl + j] = F2u;
+      Fd[(int64_t)i * nl + j] = F1d;
+      if (a.dtaus) a.dtaus[(int64_t)(k + 1) * nl + j] = dtau;
+    }
+    const double q0 = wave_sum(wt * F2u);
+    const double q1 = wave_sum(wt * F2d);
+    const double q2 = wave_sum(wt * F1u);
+    const double q3 = wave_sum(wt * F1d);
+    if (lane == 0) {
+      double* r = red + ((int64_t)wv * ns + k) * 4;
+      r[0] = q0; r[1] = q1; r[2] = q2; r[3] = q3;
+    }
+    if (DIR == kEmit) { carry = F2u; Bc = B2; } else { carry = F1d; Bc = B1; }
+  }
+  __syncthreads();
+  const int nw = kBlock / 64;
+  for (int idx = tid; idx < ns * 4; idx += kBlock) {
+    double v = red[idx];
+    for (int w = 1; w < nw; ++w) v += red[(int64_t)w * ns * 4 + idx];
+    a.part[(int64_t)idx * gridDim.x + blockIdx.x] = v;
+  }
+}
+
+// ---------------------------------------------------------------- partial sums
+__global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ part,
+                                                     int nblocks, double* __restrict__ Fb,
+                                                     const int* conv, int force) {
+  if (!force && *conv) return;
+  __shared__ double sh[256];
+  const double* p = part + (int64_t)blockIdx.x * nblocks;
+  double acc = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += 256) acc += p[b];
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) Fb[blockIdx.x] = sh[0];
+}
+
+// ---------------------------------------------------------------- setup (T -> terms)
+__device__ void setup_sweep(const SetupArgs& u, const double* T, int dir) {
+  const int nL = u.n_layers;
+  const int ns = nL - 1;
+  for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+    const int i = step_layer(dir, k, nL);
+    StepP sp;
+    sp.layer = i;
+    sp.top = (dir == kEmit && i == nL - 1) ? 1 : 0;
+    sp.T1 = T[i];
+    sp.T2 = sp.top ? T[i] : T[i + 1];                         // twostream.py:358-363
+    const double p2 = sp.top ? u.p_top2 : u.p[i + 1];
+    sp.dm = (u.p[i] - p2) / u.g;
+    sp.pad = 0;
+    u.steps[k] = sp;
+  }
+  const int nS = u.n_species;
+  for (int idx = threadIdx.x; idx < ns * nS; idx += blockDim.x) {
+    const int k = idx / nS, s = idx % nS;
+    const int i = step_layer(dir, k, nL);
+    u.terms[idx] = make_term(u.spec[s], u.pmeta[(int64_t)s * nL + i], u.tnodes, u.tperm,
+                             u.mmr[(int64_t)s * nL + i], T[i], u.fast);
+  }
+}
+
+__global__ void setup_kernel(SetupArgs u, int dir) { setup_sweep(u, u.T, dir); }
+
+// ---------------------------------------------------------------- K4/K5: update
+__device__ double layer_dT(const double* Fb, double T1, double T2, double p1, double p2,
+                           double g, double m_bar, double alpha) {
+  // div_bol_net_flux (twostream.py:190-205)
+  const double dF_rad = (Fb[0] - Fb[1]) - (Fb[2] - Fb[3]);
+  const double dz = (kKB * T1) / (m_bar * g) * log(p1 / p2);          // :180-187
+  const double cp = (2 + 5) / (2 * m_bar) * kKB;                      // :220-224
+  const double rho = ((p1 - p2) / g) / dz;                            // :234-238
+  const double dg = (T1 - T2) / dz - g / cp;                          // :241-266
+  double dF_conv = 0.0;                                               // :273-287
+  if (dg > 0) {
+    const double lmix = alpha * kKB * T1 / (m_bar * g);
+    dF_conv = rho * cp * (lmix * lmix) * sqrt(g / T1) * pow(dg, 1.5);
+  }
+  const double div = (dF_rad + dF_conv) / dz;
+  // delta_t_i (:23-43)
+  const double x = div * dz;
+  const double f = (x != 0) ? 1e5 / pow(fabs(x), 0.9) : 1.0;
+  const double dt_rad = cp * p1 / kSigmaSB / g / pow(T1, 3.0);
+  double dt;
+  if (dg > 0) {
+    const double dt_conv = sqrt(T1 / g / dg);
+    dt = f * fmin(dt_rad, dt_conv);
+  } else {
+    dt = f * dt_rad;
+  }
+  // delta_temperature with the default m_bar (:208-217, Q7)
+  const double m0 = kMbarDefault;
+  const double dz0 = (kKB * T1) / (m0 * g) * log(p1 / p2);
+  const double rho0 = ((p1 - p2) / g) / dz0;
+  const double cp0 = (2 + 5) / (2 * m0) * kKB;
+  return 1 / rho0 / cp0 * div * dt;
+}
+
+__global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
+  if (!a.force && *a.conv) return;
+  extern __shared__ double shT[];  // [n_layers] new temperatures
+  __shared__ int all_conv;
+  const int nL = a.su.n_layers;
+  const int ns = nL - 1;
+  const int dir = a.dir;
+  if (threadIdx.x == 0) all_conv = 1;
+  for (int l = threadIdx.x; l < nL; l += blockDim.x) shT[l] = 0.0;  // dT scratch
+  __syncthreads();
+  for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+    double Fb[4];
+    for (int q = 0; q < 4; ++q) {
+      double v = a.Fb[k * 4 + q];
+      for (int r = 1; r < a.nranks; ++r) v += a.Fb[(int64_t)r * ns * 4 + k * 4 + q];
+      Fb[q] = v;
+      if (a.bol_out) a.bol_out[(int64_t)step_layer(dir, k, nL) * 4 + q] = v;
+    }
+    const int i = step_layer(dir, k, nL);
+    const bool top = (dir == kEmit && i == nL - 1);
+    const double T1 = a.su.T[i];
+    const double T2 = top ? T1 : a.su.T[i + 1];
+    const double p2 = top ? a.su.p_top2 : a.su.p[i + 1];
+    shT[i] = layer_dT(Fb, T1, T2, a.su.p[i], p2, a.su.g, a.m_bar, a.alpha);
+  }
+  __syncthreads();
+  // T <- T - dT for every layer (untouched layers have dT = 0, Q6)
+  const int it = *a.iter;
+  for (int l = threadIdx.x; l < nL; l += blockDim.x) {
+    const double dT = shT[l];
+    const double Told = a.su.T[l];
+    const double Tnew = Told - dT;
+    if (a.dT_out) a.dT_out[l] = dT;
+    if (a.track) {
+      if (dir == kEmit) {
+        a.Tb[l] = Tnew;  // temperature entering the absorb sweep
+      } else {
+        // absorb history column pair [T_before, T_after] (core.py:303-307)
+        if (it < a.hist_cap) {
+          a.hist[((int64_t)it * 2 + 0) * nL + l] = a.Tb[l];
+          a.hist[((int64_t)it * 2 + 1) * nL + l] = Tnew;
+        }
+        // incremental sign-flip count over the concatenated history (core.py:308-311)
+        double dseq[2];
+        int nd = 0;
+        if (it > 0) dseq[nd++] = a.Tb[l] - a.Ta[l];
+        dseq[nd++] = Tnew - a.Tb[l];
+        for (int q = 0; q < nd; ++q) {
+          const int sgn = (dseq[q] > 0) - (dseq[q] < 0);
+          if (a.ndiff[l] > 0 && sgn != a.prev_sign[l]) a.flips[l] += 1;
+          a.prev_sign[l] = sgn;
+          a.ndiff[l] += 1;
+        }
+        a.Ta[l] = Tnew;
+        const bool c = (a.flips[l] > a.n_zero_crossings) || (fabs(dT) < a.convergence_dT);
+        if (!c) atomicAnd(&all_conv, 0);
+      }
+    }
+    a.su.T[l] = Tnew;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && a.track && dir == kAbsorb) {
+    *a.iter = it + 1;
+    if (all_conv && a.stop_on_conv) *a.conv = 1;
+  }
+  if (a.next_dir >= 0) {
+    __syncthreads();
+    setup_sweep(a.su, a.su.T, a.next_dir);
+  }
+}
+
+// ---------------------------------------------------------------- standalone kernels
+__global__ void propagate_kernel(int64_t n, const double* c1, const double* lk,
+                                 const double* F1u, const double* F2d, double T1, double T2,
+                                 const double* dtau, const double* w0, double* F2u,
+                                 double* F1d) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  double u, d;
+  two_stream(w0[j], dtau[j], planck(c1[j], lk[j], T1), planck(c1[j], lk[j], T2), F1u[j],
+             F2d[j], u, d);
+  F2u[j] = u;
+  F1d[j] = d;
+}
+
+__global__ void kappa_kernel(int64_t n, const TermP* terms, int nS, const double* sig,
+                             double* k) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  k[j] = kappa_at<1, false>(terms, nS, j, sig[j]);
+}
+
+__global__ void gen_table_kernel(double* tab, const double* base, const double* fp,
+                                 const double* fT, int n_p, int n_T, int64_t n_lam,
+                                 double lo, double hi) {
+  const int64_t total = (int64_t)n_p * n_T * n_lam;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t l = idx % n_lam;
+    const int64_t pt = idx / n_lam;
+    const int t = (int)(pt % n_T);
+    const int p = (int)(pt / n_T);
+    const double v = (fp[p] * fT[t]) * base[l];
+    tab[idx] = fmin(fmax(v, lo), hi);  // np.clip
+  }
+}
+
+__global__ void fill_kernel(double* x, int64_t n, double v) {
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+       idx += (int64_t)gridDim.x * blockDim.x)
+    x[idx] = v;
+}
+
+// ---------------------------------------------------------------- launchers
+template <int DIR, int S, bool FAST>
+static void launch_sweep_t(const SweepArgs& a, int nblocks, hipStream_t st) {
+  const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double);
+  hipLaunchKernelGGL((sweep_kernel<DIR, S, FAST>), dim3(nblocks), dim3(kBlock), shm, st, a);
+}
+
+template <int DIR>
+static void launch_sweep_dir(const SweepArgs& a, int nblocks, bool fast, hipStream_t st) {
+  if (!fast) return launch_sweep_t<DIR, 1, false>(a, nblocks, st);
+  switch (a.n_species) {
+    case 1: return launch_sweep_t<DIR, 1, true>(a, nblocks, st);
+    case 2: return launch_sweep_t<DIR, 2, true>(a, nblocks, st);
+    case 3: return launch_sweep_t<DIR, 3, true>(a, nblocks, st);
+    case 4: return launch_sweep_t<DIR, 4, true>(a, nblocks, st);
+    case 5: return launch_sweep_t<DIR, 5, true>(a, nblocks, st);
+    case 6: return launch_sweep_t<DIR, 6, true>(a, nblocks, st);
+    case 7: return launch_sweep_t<DIR, 7, true>(a, nblocks, st);
+    case 8: return launch_sweep_t<DIR, 8, true>(a, nblocks, st);
+    default: return launch_sweep_t<DIR, 1, false>(a, nblocks, st);
+  }
+}
+
+void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st) {
+  if (dir == kEmit) launch_sweep_dir<kEmit>(a, nblocks, fast, st);
+  else launch_sweep_dir<kAbsorb>(a, nblocks, fast, st);
+}
+
+void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
+                   int force, hipStream_t st) {
+  hipLaunchKernelGGL(reduce_kernel, dim3(n_idx), dim3(256), 0, st, part, nblocks, Fb, conv,
+                     force);
+}
+
+void launch_setup(const SetupArgs& u, int dir, hipStream_t st) {
+  hipLaunchKernelGGL(setup_kernel, dim3(1), dim3(256), 0, st, u, dir);
+}
+
+void launch_update(const UpdateArgs& a, hipStream_t st) {
+  const size_t shm = (size_t)a.su.n_layers * sizeof(double);
+  hipLaunchKernelGGL(update_kernel, dim3(1), dim3(256), shm, st, a);
+}
+
+void launch_propagate(int64_t n, const double* c1, const double* lk, const double* F1u,
+                      const double* F2d, double T1, double T2, const double* dtau,
+                      const double* w0, double* F2u, double* F1d, hipStream_t st) {
+  const int nb = (int)((n + 255) / 256);
+  hipLaunchKernelGGL(propagate_kernel, dim3(nb), dim3(256), 0, st, n, c1, lk, F1u, F2d, T1,
+                     T2, dtau, w0, F2u, F1d);
+}
+
+void launch_kappa(int64_t n, const TermP* terms, int nS, const double* sig, double* k,
+                  hipStream_t st) {
+  const int nb = (int)((n + 255) / 256);
+  hipLaunchKernelGGL(kappa_kernel, dim3(nb), dim3(256), 0, st, n, terms, nS, sig, k);
+}
+
+void launch_gen_table(double* tab, const double* base, const double* fp, const double* fT,
+                      int n_p, int n_T, int64_t n_lam, double lo, double hi, hipStream_t st) {
+  hipLaunchKernelGGL(gen_table_kernel, dim3(4096), dim3(256), 0, st, tab, base, fp, fT, n_p,
+                     n_T, n_lam, lo, hi);
+}
+
+void launch_fill(double* x, int64_t n, double v, hipStream_t st) {
+  const int nb = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(fill_kernel, dim3(nb > 0 ? nb : 1), dim3(256), 0, st, x, n, v);
+}
+
+}  // namespace frei

@@ -1,0 +1,872 @@
+// frei_runtime.hip — native runtime and C ABI (include/frei_hip.h) of the frei MI355X engine.
+//
+// Owns device memory, the HIP stream, the device-resident T-P loop driver (frei_run:
+// core.py:233-338), and the optional RCCL exchange of per-sweep bolometric partial sums
+// (one ncclAllGather of n_layers*4 doubles per sweep).
+#include <dlfcn.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/frei_hip.h"
+#include "frei_device.h"
+
+using namespace frei;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& msg) {
+  g_err = msg;
+  return -1;
+}
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess)                                                          \
+      return fail(std::string(#expr) + ": " + hipGetErrorString(_e));              \
+  } while (0)
+
+#define TRY(expr)                 \
+  do {                            \
+    int _r = (expr);              \
+    if (_r != 0) return _r;       \
+  } while (0)
+
+// ---------------------------------------------------------------- RCCL (dlopen)
+struct Rccl {
+  void* h = nullptr;
+  typedef int (*GetId)(void*);
+  typedef int (*InitRank)(void**, int, /*ncclUniqueId by value*/ struct Id128, int);
+  int (*getUniqueId)(void*) = nullptr;
+  int (*commInitRank)(void**, int, struct Id128, int) = nullptr;
+  int (*allGather)(const void*, void*, size_t, int, void*, hipStream_t) = nullptr;
+  int (*commDestroy)(void*) = nullptr;
+  const char* (*errStr)(int) = nullptr;
+};
+struct Id128 { char b[128]; };
+
+Rccl* rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    r.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!r.h) r.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (r.h) {
+      r.getUniqueId = (int (*)(void*))dlsym(r.h, "ncclGetUniqueId");
+      r.commInitRank = (int (*)(void**, int, Id128, int))dlsym(r.h, "ncclCommInitRank");
+      r.allGather = (int (*)(const void*, void*, size_t, int, void*, hipStream_t))dlsym(
+          r.h, "ncclAllGather");
+      r.commDestroy = (int (*)(void*))dlsym(r.h, "ncclCommDestroy");
+      r.errStr = (const char* (*)(int))dlsym(r.h, "ncclGetErrorString");
+    }
+  }
+  return (r.h && r.getUniqueId && r.commInitRank && r.allGather) ? &r : nullptr;
+}
+constexpr int kNcclFloat64 = 8;
+
+struct Species {
+  double* d_tab = nullptr;
+  int n_p = 0, n_T = 0;
+  std::vector<double> p_nodes, T_nodes;
+};
+
+}  // namespace
+
+struct frei_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int nL = 0, S = 0;
+  int64_t nlam = 0;
+  int nblocks = 0;
+  // grid
+  double *d_c1 = nullptr, *d_lk = nullptr, *d_sig = nullptr, *d_ftoa = nullptr,
+         *d_wtr = nullptr, *d_p = nullptr;
+  std::vector<double> p;
+  double p_top2 = 0, g = 0, m_bar = 0;
+  bool grid_set = false;
+  // state
+  double *d_Fu = nullptr, *d_Fd = nullptr, *d_T = nullptr, *d_dT = nullptr,
+         *d_dtaus = nullptr, *d_bol = nullptr;
+  // tables
+  std::vector<Species> sp;
+  std::vector<double> mmr;
+  bool meta_dirty = true;
+  int fast = 1;
+  SpecMeta* d_smeta = nullptr;
+  PMeta* d_pmeta = nullptr;
+  double* d_tnodes = nullptr;
+  int32_t* d_tperm = nullptr;
+  double* d_mmr = nullptr;
+  std::vector<SpecMeta> smeta;
+  std::vector<PMeta> pmeta;
+  std::vector<double> tnodes;
+  std::vector<int32_t> tperm;
+  // sweep scratch
+  StepP* d_steps = nullptr;
+  TermP* d_terms = nullptr;
+  double *d_part = nullptr, *d_Fb = nullptr, *d_Fb_all = nullptr;
+  // T-P loop state
+  int* d_conv = nullptr;
+  int* d_iter = nullptr;
+  double *d_Tb = nullptr, *d_Ta = nullptr, *d_hist = nullptr;
+  int hist_cap = 0;
+  int32_t *d_flips = nullptr, *d_prev = nullptr, *d_ndiff = nullptr;
+  int* h_flag = nullptr;  // pinned [2]
+  hipEvent_t flag_ev[2] = {nullptr, nullptr};
+  // comm
+  void* comm = nullptr;
+  int nranks = 1, rank = 0;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+};
+
+namespace {
+
+int set_device(frei_ctx* c) {
+  HIP_TRY(hipSetDevice(c->device));
+  return 0;
+}
+
+template <typename T>
+int dalloc(T** p, size_t n) {
+  if (n == 0) n = 1;
+  HIP_TRY(hipMalloc((void**)p, n * sizeof(T)));
+  return 0;
+}
+
+template <typename T>
+void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+template <typename T>
+int h2d(T* d, const T* h, size_t n, hipStream_t st) {
+  HIP_TRY(hipMemcpyAsync(d, h, n * sizeof(T), hipMemcpyHostToDevice, st));
+  return 0;
+}
+
+// Build the per-(species, layer) pressure brackets and upload all table metadata.
+int build_meta(frei_ctx* c) {
+  if (!c->meta_dirty) return 0;
+  if (!c->grid_set) return fail("frei_set_grid must be called before using tables");
+  const int nL = c->nL, S = c->S;
+  c->smeta.assign(S, SpecMeta{});
+  c->pmeta.assign((size_t)S * nL, PMeta{});
+  c->tnodes.clear();
+  c->tperm.clear();
+  int fast = 1;
+  for (int s = 0; s < S; ++s) {
+    const Species& q = c->sp[s];
+    if (!q.d_tab) return fail("opacity table of species " + std::to_string(s) + " not set");
+    SpecMeta m{};
+    m.tab = q.d_tab;
+    m.n_lam = c->nlam;
+    m.n_p = q.n_p;
+    m.n_T = q.n_T;
+    m.t_off = (int32_t)c->tnodes.size();
+    // sorted temperature nodes (xarray sortby) + permutation to memory rows
+    std::vector<int32_t> perm(q.n_T);
+    std::iota(perm.begin(), perm.end(), 0);
+    std::stable_sort(perm.begin(), perm.end(),
+                     [&](int a, int b) { return q.T_nodes[a] < q.T_nodes[b]; });
+    int n_unique = q.n_T > 0 ? 1 : 0;
+    for (int k = 1; k < q.n_T; ++k)
+      if (q.T_nodes[perm[k]] != q.T_nodes[perm[k - 1]]) ++n_unique;
+    m.one_T = (n_unique <= 1) ? 1 : 0;
+    if (!m.one_T && n_unique != q.n_T)
+      return fail("duplicate temperature nodes (drop_duplicates first, opacity.py:339)");
+    for (int k = 0; k < q.n_T; ++k) {
+      c->tnodes.push_back(q.T_nodes[perm[k]]);
+      c->tperm.push_back(perm[k]);
+    }
+    if (m.one_T) fast = 0;
+    c->smeta[s] = m;
+    // sorted pressure nodes + bracket of every layer pressure
+    std::vector<int32_t> pp(q.n_p);
+    std::iota(pp.begin(), pp.end(), 0);
+    std::stable_sort(pp.begin(), pp.end(),
+                     [&](int a, int b) { return q.p_nodes[a] < q.p_nodes[b]; });
+    std::vector<double> ps(q.n_p);
+    for (int k = 0; k < q.n_p; ++k) ps[k] = q.p_nodes[pp[k]];
+    for (int l = 0; l < nL; ++l) {
+      PMeta pm{};
+      const double x = c->p[l];
+      if (m.one_T) {
+        // scipy interp1d: searchsorted(left) clipped to [1, n-1]
+        int jx = (int)(std::lower_bound(ps.begin(), ps.end(), x) - ps.begin());
+        jx = std::max(1, std::min(jx, q.n_p - 1));
+        pm.p_lo = pp[jx - 1];
+        pm.p_hi = pp[jx];
+        pm.x1 = x - ps[jx - 1];
+        pm.dx = ps[jx] - ps[jx - 1];
+        pm.oob = (x < ps[0] || x > ps[q.n_p - 1]) ? 1 : 0;
+      } else {
+        int i, oob;
+        double y;
+        bracket(ps.data(), q.n_p, x, i, y, oob);
+        pm.p_lo = pp[i];
+        pm.p_hi = pp[i + 1];
+        pm.wp_lo = 1.0 - y;
+        pm.wp_hi = y;
+        pm.oob = oob;
+        if (!oob && pm.wp_lo != 0.0 && pm.wp_hi != 0.0) fast = 0;  // off-node pressure
+      }
+      c->pmeta[(size_t)s * nL + l] = pm;
+    }
+  }
+  c->fast = fast;
+  dfree(c->d_smeta);
+  dfree(c->d_pmeta);
+  dfree(c->d_tnodes);
+  dfree(c->d_tperm);
+  TRY(dalloc(&c->d_smeta, S));
+  TRY(dalloc(&c->d_pmeta, (size_t)S * nL));
+  TRY(dalloc(&c->d_tnodes, c->tnodes.size()));
+  TRY(dalloc(&c->d_tperm, c->tperm.size()));
+  TRY(h2d(c->d_smeta, c->smeta.data(), S, c->stream));
+  TRY(h2d(c->d_pmeta, c->pmeta.data(), (size_t)S * nL, c->stream));
+  TRY(h2d(c->d_tnodes, c->tnodes.data(), c->tnodes.size(), c->stream));
+  TRY(h2d(c->d_tperm, c->tperm.data(), c->tperm.size(), c->stream));
+  if (c->mmr.size() != (size_t)S * nL) return fail("frei_set_mmr must be called");
+  TRY(h2d(c->d_mmr, c->mmr.data(), (size_t)S * nL, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->meta_dirty = false;
+  return 0;
+}
+
+SetupArgs setup_args(frei_ctx* c) {
+  SetupArgs u{};
+  u.n_layers = c->nL;
+  u.n_species = c->S;
+  u.fast = c->fast;
+  u.T = c->d_T;
+  u.p = c->d_p;
+  u.p_top2 = c->p_top2;
+  u.g = c->g;
+  u.spec = c->d_smeta;
+  u.pmeta = c->d_pmeta;
+  u.tnodes = c->d_tnodes;
+  u.tperm = c->d_tperm;
+  u.mmr = c->d_mmr;
+  u.steps = c->d_steps;
+  u.terms = c->d_terms;
+  return u;
+}
+
+hipEvent_t next_event(frei_ctx* c) {
+  if (c->ev_used == c->ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    c->ev_pool.push_back(e);
+  }
+  return c->ev_pool[c->ev_used++];
+}
+
+struct SweepOpts {
+  int dir = kEmit;
+  int next_dir = -1;   // setup for the next sweep inside update
+  int force = 0;       // ignore the convergence flag
+  int track = 0;       // T-P history / convergence bookkeeping
+  int stop_on_conv = 0;
+  int n_zero_crossings = 2;
+  double convergence_dT = 3.0;
+  double alpha = 1.0;
+  double* dtaus = nullptr;    // device
+  double* dT_out = nullptr;   // device
+  double* bol_out = nullptr;  // device
+};
+
+// One sweep: K1 -> reduce -> [RCCL all-gather] -> K4/K5 (+ next setup).  Asynchronous.
+int run_sweep(frei_ctx* c, const SweepOpts& o) {
+  const int ns = c->nL - 1;
+  SweepArgs a{};
+  a.n_lam = c->nlam;
+  a.n_steps = ns;
+  a.n_species = c->S;
+  a.force = o.force;
+  a.c1 = c->d_c1;
+  a.lk = c->d_lk;
+  a.sig = c->d_sig;
+  a.wtr = c->d_wtr;
+  a.ftoa = c->d_ftoa;
+  a.steps = c->d_steps;
+  a.terms = c->d_terms;
+  a.F_up = c->d_Fu;
+  a.F_down = c->d_Fd;
+  a.dtaus = o.dtaus;
+  a.part = c->d_part;
+  a.conv = c->d_conv;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->timing) {
+    e0 = next_event(c);
+    e1 = next_event(c);
+    if (!e0 || !e1) return fail("hipEventCreate failed");
+    HIP_TRY(hipEventRecord(e0, c->stream));
+  }
+  launch_sweep(o.dir, a, c->nblocks, c->fast != 0, c->stream);
+  HIP_TRY(hipGetLastError());
+  if (c->timing) HIP_TRY(hipEventRecord(e1, c->stream));
+  launch_reduce(c->d_part, c->nblocks, c->d_Fb, ns * 4, c->d_conv, o.force, c->stream);
+  HIP_TRY(hipGetLastError());
+  const double* Fb = c->d_Fb;
+  if (c->nranks > 1) {
+    Rccl* r = rccl();
+    if (!r || !c->comm) return fail("RCCL communicator not initialised");
+    int rc = r->allGather(c->d_Fb, c->d_Fb_all, (size_t)ns * 4, kNcclFloat64, c->comm,
+                          c->stream);
+    if (rc != 0)
+      return fail(std::string("ncclAllGather: ") + (r->errStr ? r->errStr(rc) : "error"));
+    Fb = c->d_Fb_all;
+  }
+  UpdateArgs u{};
+  u.su = setup_args(c);
+  u.dir = o.dir;
+  u.next_dir = o.next_dir;
+  u.nranks = c->nranks;
+  u.force = o.force;
+  u.track = o.track;
+  u.stop_on_conv = o.stop_on_conv;
+  u.n_zero_crossings = o.n_zero_crossings;
+  u.hist_cap = c->hist_cap;
+  u.m_bar = c->m_bar;
+  u.alpha = o.alpha;
+  u.convergence_dT = o.convergence_dT;
+  u.Fb = Fb;
+  u.dT_out = o.dT_out;
+  u.bol_out = o.bol_out;
+  u.Tb = c->d_Tb;
+  u.Ta = c->d_Ta;
+  u.hist = c->d_hist;
+  u.flips = c->d_flips;
+  u.prev_sign = c->d_prev;
+  u.ndiff = c->d_ndiff;
+  u.iter = c->d_iter;
+  u.conv = c->d_conv;
+  launch_update(u, c->stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int reset_loop_state(frei_ctx* c) {
+  HIP_TRY(hipMemsetAsync(c->d_conv, 0, sizeof(int), c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_iter, 0, sizeof(int), c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_flips, 0, sizeof(int32_t) * c->nL, c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_prev, 0, sizeof(int32_t) * c->nL, c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_ndiff, 0, sizeof(int32_t) * c->nL, c->stream));
+  return 0;
+}
+
+int ensure_hist(frei_ctx* c, int cap) {
+  if (cap <= c->hist_cap) return 0;
+  dfree(c->d_hist);
+  TRY(dalloc(&c->d_hist, (size_t)cap * 2 * c->nL));
+  c->hist_cap = cap;
+  return 0;
+}
+
+int ensure_dtaus(frei_ctx* c) {
+  if (!c->d_dtaus) TRY(dalloc(&c->d_dtaus, (size_t)c->nL * c->nlam));
+  launch_fill(c->d_dtaus, c->nlam, 1.0, c->stream);  // row 0 placeholder (Q12)
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+bool ready(frei_ctx* c) { return c && c->grid_set; }
+
+}  // namespace
+
+// ==================================================================== C ABI
+extern "C" {
+
+int frei_version(void) { return 100; }
+
+const char* frei_last_error(void) { return g_err.c_str(); }
+
+int frei_device_count(int* n) {
+  if (!n) return fail("null argument");
+  HIP_TRY(hipGetDeviceCount(n));
+  return 0;
+}
+
+int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int n_species) {
+  if (!out) return fail("null argument");
+  *out = nullptr;
+  if (n_layers < 4 || n_layers > kMaxLayers)
+    return fail("n_layers must be in [4, 1024] (the emit top layer uses p[-3])");
+  if (n_lam < 2) return fail("n_lam must be >= 2");
+  if (n_species < 1 || n_species > 64) return fail("n_species must be in [1, 64]");
+  frei_ctx* c = new frei_ctx();
+  c->device = device;
+  c->nL = n_layers;
+  c->nlam = n_lam;
+  c->S = n_species;
+  c->sp.resize(n_species);
+  c->nblocks = (int)((n_lam + kBlock - 1) / kBlock);
+  auto bail = [&](int rc) {
+    frei_ctx_destroy(c);
+    return rc;
+  };
+  int rc;
+  if ((rc = set_device(c))) return bail(rc);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail("hipStreamCreate failed"));
+  const size_t NL = n_layers, NS = n_species, ns = n_layers - 1;
+  const size_t F = NL * (size_t)n_lam;
+  if ((rc = dalloc(&c->d_c1, n_lam)) || (rc = dalloc(&c->d_lk, n_lam)) ||
+      (rc = dalloc(&c->d_sig, n_lam)) || (rc = dalloc(&c->d_ftoa, n_lam)) ||
+      (rc = dalloc(&c->d_wtr, n_lam)) || (rc = dalloc(&c->d_p, NL)) ||
+      (rc = dalloc(&c->d_Fu, F)) || (rc = dalloc(&c->d_Fd, F)) ||
+      (rc = dalloc(&c->d_T, NL)) || (rc = dalloc(&c->d_dT, NL)) ||
+      (rc = dalloc(&c->d_bol, NL * 4)) || (rc = dalloc(&c->d_mmr, NS * NL)) ||
+      (rc = dalloc(&c->d_steps, ns)) || (rc = dalloc(&c->d_terms, ns * NS)) ||
+      (rc = dalloc(&c->d_part, ns * 4 * (size_t)c->nblocks)) ||
+      (rc = dalloc(&c->d_Fb, ns * 4)) || (rc = dalloc(&c->d_Fb_all, ns * 4)) ||
+      (rc = dalloc(&c->d_conv, 1)) || (rc = dalloc(&c->d_iter, 1)) ||
+      (rc = dalloc(&c->d_Tb, NL)) || (rc = dalloc(&c->d_Ta, NL)) ||
+      (rc = dalloc(&c->d_flips, NL)) || (rc = dalloc(&c->d_prev, NL)) ||
+      (rc = dalloc(&c->d_ndiff, NL)))
+    return bail(rc);
+  if (hipHostMalloc((void**)&c->h_flag, 2 * sizeof(int)) != hipSuccess)
+    return bail(fail("hipHostMalloc failed"));
+  for (int k = 0; k < 2; ++k)
+    if (hipEventCreateWithFlags(&c->flag_ev[k], hipEventDisableTiming) != hipSuccess)
+      return bail(fail("hipEventCreate failed"));
+  if (hipMemset(c->d_Fu, 0, F * sizeof(double)) != hipSuccess ||
+      hipMemset(c->d_Fd, 0, F * sizeof(double)) != hipSuccess ||
+      hipMemset(c->d_conv, 0, sizeof(int)) != hipSuccess)
+    return bail(fail("hipMemset failed"));
+  *out = c;
+  return 0;
+}
+
+int frei_ctx_destroy(frei_ctx* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) {
+    Rccl* r = rccl();
+    if (r && r->commDestroy) r->commDestroy(c->comm);
+  }
+  for (auto& s : c->sp) dfree(s.d_tab);
+  double* dd[] = {c->d_c1, c->d_lk, c->d_sig, c->d_ftoa, c->d_wtr, c->d_p, c->d_Fu, c->d_Fd,
+                  c->d_T, c->d_dT, c->d_dtaus, c->d_bol, c->d_tnodes, c->d_mmr, c->d_part,
+                  c->d_Fb, c->d_Fb_all, c->d_Tb, c->d_Ta, c->d_hist};
+  for (double* p : dd)
+    if (p) (void)hipFree(p);
+  void* vv[] = {c->d_smeta, c->d_pmeta, c->d_tperm, c->d_steps, c->d_terms, c->d_conv,
+                c->d_iter, c->d_flips, c->d_prev, c->d_ndiff};
+  for (void* p : vv)
+    if (p) (void)hipFree(p);
+  if (c->h_flag) (void)hipHostFree(c->h_flag);
+  for (auto e : c->flag_ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+int frei_set_grid(frei_ctx* c, const double* c1, const double* lk, const double* sigma,
+                  const double* f_toa, const double* trapz_w, const double* p, double g,
+                  double m_bar) {
+  if (!c || !c1 || !lk || !sigma || !f_toa || !trapz_w || !p) return fail("null argument");
+  if (!(g > 0) || !(m_bar > 0)) return fail("g and m_bar must be positive");
+  TRY(set_device(c));
+  const int64_t n = c->nlam;
+  c->p.assign(p, p + c->nL);
+  for (int l = 1; l < c->nL; ++l)
+    if (!(c->p[l] < c->p[l - 1])) return fail("pressures must be strictly descending (BOA first)");
+  // emit's top layer: p_2 = p[-1] * p[-2] / p[-3] (twostream.py:359)
+  c->p_top2 = c->p[c->nL - 1] * c->p[c->nL - 2] / c->p[c->nL - 3];
+  c->g = g;
+  c->m_bar = m_bar;
+  TRY(h2d(c->d_c1, c1, n, c->stream));
+  TRY(h2d(c->d_lk, lk, n, c->stream));
+  TRY(h2d(c->d_sig, sigma, n, c->stream));
+  TRY(h2d(c->d_ftoa, f_toa, n, c->stream));
+  TRY(h2d(c->d_wtr, trapz_w, n, c->stream));
+  TRY(h2d(c->d_p, c->p.data(), c->nL, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->grid_set = true;
+  c->meta_dirty = true;
+  return 0;
+}
+
+static int set_table_common(frei_ctx* c, int s, const double* p_nodes, int n_p,
+                            const double* T_nodes, int n_T) {
+  if (s < 0 || s >= c->S) return fail("species index out of range");
+  if (n_p < 2) return fail("a table needs at least 2 pressure nodes");
+  if (n_T < 1) return fail("a table needs at least 1 temperature node");
+  Species& q = c->sp[s];
+  const size_t need = (size_t)n_p * n_T * (size_t)c->nlam;
+  if (!q.d_tab || (size_t)q.n_p * q.n_T != (size_t)n_p * n_T) {
+    dfree(q.d_tab);
+    TRY(dalloc(&q.d_tab, need));
+  }
+  q.n_p = n_p;
+  q.n_T = n_T;
+  q.p_nodes.assign(p_nodes, p_nodes + n_p);
+  q.T_nodes.assign(T_nodes, T_nodes + n_T);
+  c->meta_dirty = true;
+  return 0;
+}
+
+int frei_set_table(frei_ctx* c, int s, const double* values, const double* p_nodes, int n_p,
+                   const double* T_nodes, int n_T) {
+  if (!c || !values || !p_nodes || !T_nodes) return fail("null argument");
+  TRY(set_device(c));
+  TRY(set_table_common(c, s, p_nodes, n_p, T_nodes, n_T));
+  const size_t need = (size_t)n_p * n_T * (size_t)c->nlam;
+  HIP_TRY(hipMemcpy(c->sp[s].d_tab, values, need * sizeof(double), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int frei_set_table_separable(frei_ctx* c, int s, const double* base, const double* fp,
+                             const double* fT, double lo, double hi, const double* p_nodes,
+                             int n_p, const double* T_nodes, int n_T) {
+  if (!c || !base || !fp || !fT || !p_nodes || !T_nodes) return fail("null argument");
+  TRY(set_device(c));
+  TRY(set_table_common(c, s, p_nodes, n_p, T_nodes, n_T));
+  double *d_base = nullptr, *d_fp = nullptr, *d_fT = nullptr;
+  TRY(dalloc(&d_base, c->nlam));
+  TRY(dalloc(&d_fp, n_p));
+  TRY(dalloc(&d_fT, n_T));
+  TRY(h2d(d_base, base, c->nlam, c->stream));
+  TRY(h2d(d_fp, fp, n_p, c->stream));
+  TRY(h2d(d_fT, fT, n_T, c->stream));
+  launch_gen_table(c->sp[s].d_tab, d_base, d_fp, d_fT, n_p, n_T, c->nlam, lo, hi, c->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  dfree(d_base);
+  dfree(d_fp);
+  dfree(d_fT);
+  return 0;
+}
+
+int frei_set_mmr(frei_ctx* c, const double* mmr) {
+  if (!c || !mmr) return fail("null argument");
+  c->mmr.assign(mmr, mmr + (size_t)c->S * c->nL);
+  c->meta_dirty = true;
+  return 0;
+}
+
+int frei_set_fluxes(frei_ctx* c, const double* up, const double* down) {
+  if (!c) return fail("null argument");
+  TRY(set_device(c));
+  const size_t F = (size_t)c->nL * c->nlam;
+  if (up) TRY(h2d(c->d_Fu, up, F, c->stream));
+  if (down) TRY(h2d(c->d_Fd, down, F, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int frei_get_fluxes(frei_ctx* c, double* up, double* down) {
+  if (!c) return fail("null argument");
+  TRY(set_device(c));
+  const size_t F = (size_t)c->nL * c->nlam;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (up) HIP_TRY(hipMemcpy(up, c->d_Fu, F * sizeof(double), hipMemcpyDeviceToHost));
+  if (down) HIP_TRY(hipMemcpy(down, c->d_Fd, F * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int frei_set_temperatures(frei_ctx* c, const double* T) {
+  if (!c || !T) return fail("null argument");
+  for (int l = 0; l < c->nL; ++l)
+    if (!(T[l] > 0)) return fail("temperatures must be positive");
+  TRY(set_device(c));
+  TRY(h2d(c->d_T, T, c->nL, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int frei_get_temperatures(frei_ctx* c, double* T) {
+  if (!c || !T) return fail("null argument");
+  TRY(set_device(c));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(T, c->d_T, c->nL * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int frei_sweep(frei_ctx* c, int direction, double alpha, double* dT, double* bol,
+               double* dtaus) {
+  if (!ready(c)) return fail("context not ready (frei_set_grid)");
+  if (direction != FREI_EMIT && direction != FREI_ABSORB) return fail("bad direction");
+  TRY(set_device(c));
+  TRY(build_meta(c));
+  SweepOpts o;
+  o.dir = direction;
+  o.force = 1;
+  o.alpha = alpha;
+  o.dT_out = c->d_dT;
+  o.bol_out = c->d_bol;
+  if (dtaus) {
+    TRY(ensure_dtaus(c));
+    o.dtaus = c->d_dtaus;
+  }
+  launch_setup(setup_args(c), direction, c->stream);
+  HIP_TRY(hipGetLastError());
+  TRY(run_sweep(c, o));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (dT) HIP_TRY(hipMemcpy(dT, c->d_dT, c->nL * sizeof(double), hipMemcpyDeviceToHost));
+  if (bol) {
+    HIP_TRY(hipMemcpy(bol, c->d_bol, c->nL * 4 * sizeof(double), hipMemcpyDeviceToHost));
+    // rows of layers a sweep does not visit are undefined on the device: zero them
+    const int skip = (direction == FREI_EMIT) ? 0 : c->nL - 1;
+    for (int q = 0; q < 4; ++q) bol[skip * 4 + q] = 0.0;
+  }
+  if (dtaus)
+    HIP_TRY(hipMemcpy(dtaus, c->d_dtaus, (size_t)c->nL * c->nlam * sizeof(double),
+                      hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int frei_state_init(frei_ctx* c, const double* T_init) {
+  if (!ready(c) || !T_init) return fail("context not ready or null T_init");
+  TRY(set_device(c));
+  TRY(build_meta(c));
+  TRY(frei_set_temperatures(c, T_init));
+  const size_t F = (size_t)c->nL * c->nlam;
+  HIP_TRY(hipMemsetAsync(c->d_Fu, 0, F * sizeof(double), c->stream));  // core.py:265-266
+  HIP_TRY(hipMemsetAsync(c->d_Fd, 0, F * sizeof(double), c->stream));
+  TRY(reset_loop_state(c));
+  launch_setup(setup_args(c), kEmit, c->stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+static int iterate(frei_ctx* c, int n, int nzc, double thr, double alpha, bool stop) {
+  for (int it = 0; it < n; ++it) {
+    SweepOpts e;
+    e.dir = kEmit;
+    e.next_dir = kAbsorb;
+    e.track = 1;
+    e.alpha = alpha;
+    TRY(run_sweep(c, e));
+    SweepOpts a = e;
+    a.dir = kAbsorb;
+    a.next_dir = kEmit;
+    a.stop_on_conv = stop ? 1 : 0;
+    a.n_zero_crossings = nzc;
+    a.convergence_dT = thr;
+    TRY(run_sweep(c, a));
+  }
+  return 0;
+}
+
+int frei_iterate(frei_ctx* c, int n, int n_zero_crossings, double convergence_dT,
+                 double alpha) {
+  if (!ready(c)) return fail("context not ready");
+  TRY(set_device(c));
+  TRY(ensure_hist(c, 1));
+  const bool stop = n_zero_crossings >= 0;
+  return iterate(c, n, stop ? n_zero_crossings : 0x7fffffff, convergence_dT, alpha, stop);
+}
+
+int frei_synchronize(frei_ctx* c) {
+  if (!c) return fail("null argument");
+  TRY(set_device(c));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int frei_run(frei_ctx* c, const double* T_init, int n_timesteps, int n_zero_crossings,
+             double convergence_dT, double alpha, int* n_iter, double* T_final,
+             double* temp_hist, double* dtaus, double* spectrum) {
+  if (!ready(c) || !T_init || !n_iter) return fail("context not ready or null argument");
+  if (n_timesteps < 1) return fail("n_timesteps must be >= 1");
+  TRY(set_device(c));
+  TRY(ensure_hist(c, n_timesteps));
+  TRY(frei_state_init(c, T_init));
+  // device-resident loop; poll the convergence flag one chunk behind
+  const int chunk = 4;
+  int launched = 0, k = 0;
+  while (launched < n_timesteps) {
+    const int n = std::min(chunk, n_timesteps - launched);
+    TRY(iterate(c, n, n_zero_crossings, convergence_dT, alpha, true));
+    launched += n;
+    HIP_TRY(hipMemcpyAsync(&c->h_flag[k & 1], c->d_conv, sizeof(int), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipEventRecord(c->flag_ev[k & 1], c->stream));
+    if (k > 0) {
+      HIP_TRY(hipEventSynchronize(c->flag_ev[(k - 1) & 1]));
+      if (c->h_flag[(k - 1) & 1]) break;
+    }
+    ++k;
+  }
+  // final emit without alpha (alpha = 1, core.py:323-333), writes dtaus
+  TRY(ensure_dtaus(c));
+  SweepOpts f;
+  f.dir = kEmit;
+  f.force = 1;
+  f.alpha = 1.0;
+  f.dtaus = c->d_dtaus;
+  TRY(run_sweep(c, f));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  int it = 0;
+  HIP_TRY(hipMemcpy(&it, c->d_iter, sizeof(int), hipMemcpyDeviceToHost));
+  *n_iter = it;
+  const int nL = c->nL;
+  if (T_final) HIP_TRY(hipMemcpy(T_final, c->d_T, nL * sizeof(double), hipMemcpyDeviceToHost));
+  if (temp_hist && it > 0) {
+    std::vector<double> h((size_t)it * 2 * nL);
+    HIP_TRY(hipMemcpy(h.data(), c->d_hist, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int l = 0; l < nL; ++l)
+      for (int col = 0; col < 2 * it; ++col) temp_hist[(size_t)l * 2 * it + col] = h[(size_t)col * nL + l];
+  }
+  if (dtaus)
+    HIP_TRY(hipMemcpy(dtaus, c->d_dtaus, (size_t)nL * c->nlam * sizeof(double),
+                      hipMemcpyDeviceToHost));
+  if (spectrum)
+    HIP_TRY(hipMemcpy(spectrum, c->d_Fu + (size_t)(nL - 1) * c->nlam, c->nlam * sizeof(double),
+                      hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int frei_kappa(frei_ctx* c, double T, double p, double* k, double* sigma) {
+  if (!ready(c) || !k) return fail("context not ready or null argument");
+  TRY(set_device(c));
+  TRY(build_meta(c));
+  std::vector<TermP> terms(c->S);
+  for (int s = 0; s < c->S; ++s) {
+    const Species& q = c->sp[s];
+    const SpecMeta& sm = c->smeta[s];
+    // pressure bracket of the query point (same rules as build_meta)
+    std::vector<int32_t> pp(q.n_p);
+    std::iota(pp.begin(), pp.end(), 0);
+    std::stable_sort(pp.begin(), pp.end(),
+                     [&](int a, int b) { return q.p_nodes[a] < q.p_nodes[b]; });
+    std::vector<double> ps(q.n_p);
+    for (int i = 0; i < q.n_p; ++i) ps[i] = q.p_nodes[pp[i]];
+    PMeta pm{};
+    if (sm.one_T) {
+      int jx = (int)(std::lower_bound(ps.begin(), ps.end(), p) - ps.begin());
+      jx = std::max(1, std::min(jx, q.n_p - 1));
+      pm.p_lo = pp[jx - 1];
+      pm.p_hi = pp[jx];
+      pm.x1 = p - ps[jx - 1];
+      pm.dx = ps[jx] - ps[jx - 1];
+      pm.oob = (p < ps[0] || p > ps[q.n_p - 1]) ? 1 : 0;
+    } else {
+      int i, oob;
+      double y;
+      bracket(ps.data(), q.n_p, p, i, y, oob);
+      pm.p_lo = pp[i];
+      pm.p_hi = pp[i + 1];
+      pm.wp_lo = 1.0 - y;
+      pm.wp_hi = y;
+      pm.oob = oob;
+    }
+    // mmr: the layer whose pressure equals p, else the first layer's value
+    double m = c->mmr[(size_t)s * c->nL];
+    for (int l = 0; l < c->nL; ++l)
+      if (c->p[l] == p) m = c->mmr[(size_t)s * c->nL + l];
+    terms[s] = make_term(sm, pm, c->tnodes.data(), c->tperm.data(), m, T, 0);
+  }
+  TermP* d_terms = nullptr;
+  double* d_k = nullptr;
+  TRY(dalloc(&d_terms, c->S));
+  TRY(dalloc(&d_k, c->nlam));
+  TRY(h2d(d_terms, terms.data(), c->S, c->stream));
+  launch_kappa(c->nlam, d_terms, c->S, c->d_sig, d_k, c->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(k, d_k, c->nlam * sizeof(double), hipMemcpyDeviceToHost));
+  if (sigma) HIP_TRY(hipMemcpy(sigma, c->d_sig, c->nlam * sizeof(double), hipMemcpyDeviceToHost));
+  dfree(d_terms);
+  dfree(d_k);
+  return 0;
+}
+
+int frei_propagate_fluxes(int device, int64_t n, const double* c1, const double* lk,
+                          const double* F_1_up, const double* F_2_down, double T_1,
+                          double T_2, const double* delta_tau, const double* omega_0,
+                          double* F_2_up, double* F_1_down) {
+  if (n <= 0) return 0;
+  if (!c1 || !lk || !F_1_up || !F_2_down || !delta_tau || !omega_0 || !F_2_up || !F_1_down)
+    return fail("null argument");
+  HIP_TRY(hipSetDevice(device));
+  double* d[10] = {};
+  for (int i = 0; i < 10; ++i) TRY(dalloc(&d[i], n));
+  const double* in[6] = {c1, lk, F_1_up, F_2_down, delta_tau, omega_0};
+  for (int i = 0; i < 6; ++i)
+    HIP_TRY(hipMemcpy(d[i], in[i], n * sizeof(double), hipMemcpyHostToDevice));
+  launch_propagate(n, d[0], d[1], d[2], d[3], T_1, T_2, d[4], d[5], d[6], d[7], nullptr);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(F_2_up, d[6], n * sizeof(double), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(F_1_down, d[7], n * sizeof(double), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 10; ++i) dfree(d[i]);
+  return 0;
+}
+
+int frei_comm_unique_id(void* id128) {
+  if (!id128) return fail("null argument");
+  Rccl* r = rccl();
+  if (!r) return fail("librccl.so.1 not loadable");
+  int rc = r->getUniqueId(id128);
+  if (rc != 0) return fail("ncclGetUniqueId failed");
+  return 0;
+}
+
+int frei_comm_init(frei_ctx* c, int nranks, int rank, const void* id128) {
+  if (!c || !id128) return fail("null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail("bad rank/nranks");
+  TRY(set_device(c));
+  if (nranks == 1) {
+    c->nranks = 1;
+    c->rank = 0;
+    return 0;
+  }
+  Rccl* r = rccl();
+  if (!r) return fail("librccl.so.1 not loadable");
+  Id128 id;
+  std::memcpy(id.b, id128, 128);
+  void* comm = nullptr;
+  int rc = r->commInitRank(&comm, nranks, id, rank);
+  if (rc != 0)
+    return fail(std::string("ncclCommInitRank: ") + (r->errStr ? r->errStr(rc) : "error"));
+  c->comm = comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  dfree(c->d_Fb_all);
+  TRY(dalloc(&c->d_Fb_all, (size_t)nranks * (c->nL - 1) * 4));
+  return 0;
+}
+
+int frei_timing_enable(frei_ctx* c, int on) {
+  if (!c) return fail("null argument");
+  TRY(set_device(c));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->timing = on != 0;
+  c->ev_used = 0;
+  return 0;
+}
+
+int frei_timing_read(frei_ctx* c, double* total_ms, int* n_launches) {
+  if (!c || !total_ms || !n_launches) return fail("null argument");
+  TRY(set_device(c));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  double tot = 0;
+  for (size_t k = 0; k + 1 < c->ev_used; k += 2) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev_pool[k], c->ev_pool[k + 1]));
+    tot += ms;
+  }
+  *total_ms = tot;
+  *n_launches = (int)(c->ev_used / 2);
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,229 @@
+"""Host driver of one GPU context (one ``frei_ctx`` of include/frei_hip.h).
+
+An :class:`Engine` owns a contiguous wavelength slice of a global grid on one device:
+it precomputes the per-wavelength constants of the reference's setup (Planck prefactor,
+Rayleigh sigma, F_TOA, trapezoid weights — core.py:48-62, opacity.py:173-200,
+twostream.py:16-20, 46-67) with NumPy on the host, uploads the opacity tables and mmr,
+and calls the HIP kernels for sweeps, the T-P loop and kappa.  Nothing here computes
+fluxes on the CPU: without libfrei_hip.so every call raises.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .chemistry import chemistry
+from .constants import BAR, C, H, K_B, M_BAR_DEFAULT, UM
+from .opacity import SeparableTable, sigma_scattering
+from .units import scalar, value
+
+EMIT, ABSORB = 0, 1
+
+
+def planck_prefactor(lam_cm):
+    """2 h c^2 / lam^5 exactly as BB forms it (twostream.py:64-66)."""
+    return 2 * H * C ** 2 / np.power(lam_cm, 5)
+
+
+def bb(T, lam_um):
+    lam_cm = np.asarray(lam_um, dtype=float) * UM
+    return planck_prefactor(lam_cm) / np.expm1(H * C / (lam_cm * K_B * T))
+
+
+def f_toa(lam_um, T_star=5800.0, f=2 / 3, a_rstar=6.450964670116429):
+    """Stellar flux at the top of the atmosphere, erg s^-1 cm^-3 (core.py:48-55)."""
+    return f * a_rstar ** -2 * 1 / (2 * np.pi) * (np.pi * bb(T_star, lam_um))
+
+
+def trapz_weights(lam_cm):
+    """Per-point trapezoid weights of np.trapz on the global grid, so a wavelength slice
+    contributes sum(w*F) with no halo."""
+    d = np.diff(lam_cm)
+    w = np.zeros(lam_cm.size)
+    w[:-1] += d / 2
+    w[1:] += d / 2
+    return w
+
+
+def partition(n, nranks, rank):
+    """Contiguous, balanced wavelength slice [lo, hi) of rank ``rank``."""
+    base, rem = divmod(n, nranks)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def _table_arrays(tab):
+    p = np.asarray(value(tab.pressure, "bar"), dtype=float)
+    T = np.asarray(value(tab.temperature, "K"), dtype=float)
+    return p, T
+
+
+class Engine:
+    """One device context for the wavelength slice ``lam_slice`` of ``lam_um``.
+
+    Parameters mirror the reference's Grid/Planet: ``p_bar`` layer pressures (bar,
+    descending), ``opacities`` dict of tables, ``g`` (cm s^-2), ``m_bar`` (g),
+    ``F_toa`` (erg s^-1 cm^-3, global grid) and ``mmr`` [n_species][n_layers]
+    (default: the reference's mock chemistry, chemistry.py:207-246).
+    """
+
+    def __init__(self, lam_um, p_bar, opacities, g=2478.6519476149147, m_bar=M_BAR_DEFAULT,
+                 F_toa=None, mmr=None, device=0, lam_slice=None, comm=None):
+        lib = N.lib()
+        self.lam_um = np.asarray(value(lam_um, "um"), dtype=float)
+        self.p_bar = np.asarray(value(p_bar, "bar"), dtype=float)
+        self.g = scalar(g, "cm / s2")
+        self.m_bar = scalar(m_bar, "g")
+        self.names = list(opacities)
+        self.n_layers = self.p_bar.size
+        n = self.lam_um.size
+        lo, hi = lam_slice if lam_slice is not None else (0, n)
+        self.lo, self.hi = lo, hi
+        self.n_lam = hi - lo
+        self.device = device
+        lam_cm = self.lam_um * UM
+        sl = slice(lo, hi)
+        self.c1 = N.f64(planck_prefactor(lam_cm)[sl])
+        self.lk = N.f64((lam_cm * K_B)[sl])
+        self.sigma = N.f64(sigma_scattering(self.lam_um, self.m_bar)[sl])
+        ft = f_toa(self.lam_um) if F_toa is None else value(F_toa, "erg / (s cm3)")
+        self.f_toa = N.f64(np.asarray(ft, dtype=float)[sl])
+        self.wtr = N.f64(trapz_weights(lam_cm)[sl])
+        self.p_cgs = N.f64(self.p_bar * BAR)
+        ctx = ctypes.c_void_p()
+        N.check(lib.frei_ctx_create(ctypes.byref(ctx), device, self.n_layers, self.n_lam,
+                                    len(self.names)))
+        self._ctx = ctx
+        N.check(lib.frei_set_grid(ctx, N.dptr(self.c1), N.dptr(self.lk), N.dptr(self.sigma),
+                                  N.dptr(self.f_toa), N.dptr(self.wtr), N.dptr(self.p_cgs),
+                                  self.g, self.m_bar))
+        for s, name in enumerate(self.names):
+            self._set_table(s, opacities[name], sl)
+        if mmr is None:
+            T0 = np.full(self.n_layers, 1000.0)
+            mm = chemistry(T0, self.p_bar, self.names, m_bar=self.m_bar)
+            mmr = np.array([mm[nm] for nm in self.names])
+        self.mmr = N.f64(np.broadcast_to(np.asarray(mmr, dtype=float),
+                                         (len(self.names), self.n_layers)))
+        N.check(lib.frei_set_mmr(ctx, N.dptr(self.mmr)))
+        if comm is not None:
+            nranks, rank, uid = comm
+            buf = ctypes.create_string_buffer(bytes(uid), 128)
+            N.check(lib.frei_comm_init(ctx, nranks, rank, buf))
+
+    # ------------------------------------------------------------------ setup
+    def _set_table(self, s, tab, sl):
+        lib = N.lib()
+        p, T = _table_arrays(tab)
+        p_cgs, T = N.f64(p * BAR), N.f64(T)
+        if isinstance(tab, SeparableTable):
+            N.check(lib.frei_set_table_separable(
+                self._ctx, s, N.dptr(N.f64(tab.base[sl])), N.dptr(N.f64(tab.fp)),
+                N.dptr(N.f64(tab.fT)), tab.lo, tab.hi, N.dptr(p_cgs), p.size, N.dptr(T), T.size))
+            return
+        vals = np.asarray(tab.values)
+        if vals.ndim != 3 or vals.shape[:2] != (p.size, T.size):
+            raise ValueError("opacity table must be (pressure, temperature, wavelength)")
+        if vals.shape[2] != self.lam_um.size:
+            raise ValueError("opacity table wavelength axis must match the grid")
+        v = N.f64(vals[:, :, sl])
+        N.check(lib.frei_set_table(self._ctx, s, N.dptr(v), N.dptr(p_cgs), p.size,
+                                   N.dptr(T), T.size))
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            N.lib().frei_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ state
+    def set_fluxes(self, up=None, down=None):
+        N.check(N.lib().frei_set_fluxes(self._ctx, N.dptr(None if up is None else N.f64(up)),
+                                        N.dptr(None if down is None else N.f64(down))))
+
+    def get_fluxes(self):
+        up = np.empty((self.n_layers, self.n_lam))
+        down = np.empty((self.n_layers, self.n_lam))
+        N.check(N.lib().frei_get_fluxes(self._ctx, N.dptr(up), N.dptr(down)))
+        return up, down
+
+    def set_temperatures(self, T):
+        N.check(N.lib().frei_set_temperatures(self._ctx, N.dptr(N.f64(T))))
+
+    def get_temperatures(self):
+        T = np.empty(self.n_layers)
+        N.check(N.lib().frei_get_temperatures(self._ctx, N.dptr(T)))
+        return T
+
+    # ------------------------------------------------------------------ compute
+    def sweep(self, direction, alpha=1.0, want_dtaus=True):
+        """One emit/absorb sweep on the device state -> (dT, bolometric[n_layers][4], dtaus)."""
+        dT = np.empty(self.n_layers)
+        bol = np.empty((self.n_layers, 4))
+        dtaus = np.empty((self.n_layers, self.n_lam)) if want_dtaus else None
+        N.check(N.lib().frei_sweep(self._ctx, direction, float(alpha), N.dptr(dT), N.dptr(bol),
+                                   N.dptr(dtaus)))
+        return dT, bol, dtaus
+
+    def run(self, T_init, n_timesteps=1, n_zero_crossings=2, convergence_dT=3.0, alpha=1.0,
+            want_dtaus=True):
+        """Grid.emission_spectrum on the device (core.py:233-338)."""
+        nL = self.n_layers
+        n_iter = ctypes.c_int(0)
+        T_final = np.empty(nL)
+        hist = np.empty(nL * 2 * n_timesteps)
+        dtaus = np.empty((nL, self.n_lam)) if want_dtaus else None
+        spec = np.empty(self.n_lam)
+        N.check(N.lib().frei_run(self._ctx, N.dptr(N.f64(T_init)), int(n_timesteps),
+                                 int(n_zero_crossings), float(convergence_dT), float(alpha),
+                                 ctypes.byref(n_iter), N.dptr(T_final), N.dptr(hist),
+                                 N.dptr(dtaus), N.dptr(spec)))
+        it = n_iter.value
+        temp_hist = hist[: nL * 2 * it].reshape(nL, 2 * it)
+        return dict(spectrum=spec, final_T=T_final, temp_hist=temp_hist, dtaus=dtaus, n_iter=it)
+
+    def state_init(self, T_init):
+        N.check(N.lib().frei_state_init(self._ctx, N.dptr(N.f64(T_init))))
+
+    def iterate(self, n, n_zero_crossings=-1, convergence_dT=3.0, alpha=1.0):
+        N.check(N.lib().frei_iterate(self._ctx, int(n), int(n_zero_crossings),
+                                     float(convergence_dT), float(alpha)))
+
+    def synchronize(self):
+        N.check(N.lib().frei_synchronize(self._ctx))
+
+    def timing(self, on):
+        N.check(N.lib().frei_timing_enable(self._ctx, 1 if on else 0))
+
+    def timing_read(self):
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int(0)
+        N.check(N.lib().frei_timing_read(self._ctx, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def kappa(self, T, p_bar):
+        k = np.empty(self.n_lam)
+        sig = np.empty(self.n_lam)
+        N.check(N.lib().frei_kappa(self._ctx, float(T), float(p_bar) * BAR, N.dptr(k),
+                                   N.dptr(sig)))
+        return k, sig
+
+
+def propagate_fluxes_device(lam_um, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0, device=0):
+    """twostream.py:97-177 on the GPU (g_0 = 0)."""
+    lam_cm = np.asarray(lam_um, dtype=float).ravel() * UM
+    n = lam_cm.size
+    bc = lambda a: N.f64(np.broadcast_to(np.asarray(a, dtype=float).ravel()
+                                         if np.ndim(a) else a, (n,)))
+    c1, lk = N.f64(planck_prefactor(lam_cm)), N.f64(lam_cm * K_B)
+    F1u, F2d, dtau, w0 = bc(F_1_up), bc(F_2_down), bc(delta_tau), bc(omega_0)
+    F2u, F1d = np.empty(n), np.empty(n)
+    N.check(N.lib().frei_propagate_fluxes(device, n, N.dptr(c1), N.dptr(lk), N.dptr(F1u),
+                                          N.dptr(F2d), float(T_1), float(T_2), N.dptr(dtau),
+                                          N.dptr(w0), N.dptr(F2u), N.dptr(F1d)))
+    return F2u, F1d

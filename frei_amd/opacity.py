@@ -1,0 +1,140 @@
+"""Opacity tables, Rayleigh scattering and ``kappa`` (frei/opacity.py).
+
+Tables are the reference's ``{isotopologue: DataArray(pressure, temperature, wavelength)}``
+dict (opacity.py:272-342); here the value type is :class:`OpacityTable` (any object
+with ``.values``, ``.pressure`` [bar], ``.temperature`` [K] works, e.g. an xarray
+DataArray).  ``kappa`` evaluates on the GPU through the C ABI (frei_kappa).
+"""
+import numpy as np
+
+from .constants import M_BAR_DEFAULT, UM
+from .units import scalar, value
+
+__all__ = ["OpacityTable", "SeparableTable", "kappa", "load_example_opacity",
+           "rayleigh_H2", "rayleigh_He", "binned_opacity"]
+
+N_REF_H2 = 2.68678e19   # cm^-3, opacity.py:23
+N_REF_HE = 2.546899e19  # cm^-3, opacity.py:24
+
+
+class OpacityTable:
+    """(pressure, temperature, wavelength) opacity grid in cm^2 g^-1."""
+
+    dims = ("pressure", "temperature", "wavelength")
+
+    def __init__(self, values, pressure, temperature, wavelength=None):
+        self.values = np.asarray(values, dtype=np.float64)
+        self.pressure = np.asarray(value(pressure, "bar"), dtype=np.float64)
+        self.temperature = np.asarray(value(temperature, "K"), dtype=np.float64)
+        self.wavelength = None if wavelength is None else np.asarray(value(wavelength, "um"))
+        if self.values.shape[:2] != (self.pressure.size, self.temperature.size):
+            raise ValueError("values must be (n_pressure, n_temperature, n_wavelength)")
+
+    @property
+    def shape(self):
+        return self.values.shape
+
+    def drop_duplicates(self, dim="temperature"):
+        """Keep the first of repeated temperature nodes (xarray drop_duplicates)."""
+        if dim != "temperature":
+            raise ValueError("only temperature duplicates are dropped")
+        _, idx = np.unique(self.temperature, return_index=True)
+        idx = np.sort(idx)
+        return OpacityTable(self.values[:, idx], self.pressure, self.temperature[idx],
+                            self.wavelength)
+
+
+class SeparableTable:
+    """Synthetic table generated on the device: clip((fp[p] * fT[T]) * base[lam], lo, hi).
+    Used for large benchmark grids (no host copy of the n_p*n_T*n_lam values)."""
+
+    def __init__(self, base, fp, fT, pressure, temperature, lo=1e-4, hi=1e3):
+        self.base = np.ascontiguousarray(base, dtype=np.float64)
+        self.fp = np.ascontiguousarray(fp, dtype=np.float64)
+        self.fT = np.ascontiguousarray(fT, dtype=np.float64)
+        self.pressure = np.asarray(value(pressure, "bar"), dtype=np.float64)
+        self.temperature = np.asarray(value(temperature, "K"), dtype=np.float64)
+        self.lo, self.hi = float(lo), float(hi)
+
+    @property
+    def values(self):  # materialise on the host (small grids / tests only)
+        return np.clip((self.fp[:, None] * self.fT[None, :])[:, :, None] * self.base[None, None, :],
+                       self.lo, self.hi)
+
+
+def n_lambda_H2(lam_um):
+    """Malik 2017 Eqn 17 (opacity.py:173-177); lam in µm."""
+    return 13.58e-5 * (1 + (7.52e-11 * np.asarray(lam_um) ** -2) * 1e8) + 1
+
+
+def n_lambda_He(lam_um):
+    """Deitrick 2020 Eqn C3 (opacity.py:180-184); lam in µm."""
+    return 1e-8 * (2283 + (1.8102e13 / (1.5342e10 - np.asarray(lam_um) ** -2))) + 1
+
+
+def _rayleigh(n, n_ref, lam_cm, m_bar):
+    return (24 * np.pi ** 3 / n_ref ** 2 / lam_cm ** 4 *
+            ((n ** 2 - 1) / (n ** 2 + 2)) ** 2 * 1) / m_bar
+
+
+def rayleigh_H2(wavelength, m_bar=M_BAR_DEFAULT):
+    """Rayleigh cross-section per unit mass, cm^2 g^-1 (opacity.py:187-192); lam in µm."""
+    lam = value(wavelength, "um")
+    return _rayleigh(n_lambda_H2(lam), N_REF_H2, lam * UM, scalar(m_bar, "g"))
+
+
+def rayleigh_He(wavelength, m_bar=M_BAR_DEFAULT):
+    """(opacity.py:195-200)"""
+    lam = value(wavelength, "um")
+    return _rayleigh(n_lambda_He(lam), N_REF_HE, lam * UM, scalar(m_bar, "g"))
+
+
+def sigma_scattering(lam_um, m_bar):
+    """rayleigh_H2 + rayleigh_He (opacity.py:233)."""
+    return rayleigh_H2(lam_um, m_bar) + rayleigh_He(lam_um, m_bar)
+
+
+def kappa(opacities, temperature, pressure, lam, m_bar=M_BAR_DEFAULT, device=0):
+    """Total opacity at one (T, p): (k, sigma_scattering) in cm^2 g^-1 (opacity.py:203-269).
+
+    k = sum_s mmr_s * interp_s(p, T) + sigma (linear, fill 0 outside the node hull;
+    pressure-only for single-temperature tables).  Runs on the GPU."""
+    from .engine import Engine
+    lam_um = value(lam, "um")
+    T = scalar(temperature, "K")
+    p = scalar(pressure, "bar")
+    eng = Engine(lam_um, np.array([p * 4, p * 2, p, p / 2]), opacities, m_bar=m_bar,
+                 device=device)
+    try:
+        return eng.kappa(T, p)
+    finally:
+        eng.close()
+
+
+def load_example_opacity(grid, seed=42, scale_factor=20):
+    """Synthetic "example" water opacity (opacity.py:272-342): broad IR/optical bands,
+    15 random optical lines (np.random.seed(seed)) and 3 NIR bands, identical at every
+    (p, T) node of ``grid``."""
+    lam = np.asarray(grid.lam, dtype=float)
+    np.random.seed(seed)
+    so = (np.exp(-0.5 * (lam - 6) ** 2 / 2 ** 2) +
+          0.8 * np.exp(-0.5 * (lam - 0.3) ** 2 / 0.5 ** 2))
+    for amp, wl in zip(np.random.uniform(low=0.1, high=0.2, size=15),
+                       np.random.uniform(low=0.5, high=1, size=15)):
+        so += amp * np.exp(-0.5 * (lam - wl) ** 2 / 0.005 ** 2)
+    for amp, wl in zip([0.22, 0.2, 0.18], np.logspace(np.log10(1.4), np.log10(2.7), 3)):
+        so += amp * np.exp(-0.5 * (lam - wl) ** 2 / 0.13 ** 2)
+    row = np.zeros(lam.size)
+    row += 5 * 10 ** (2.5 * (so - 0.4))
+    row *= scale_factor
+    p = np.asarray(grid.pressures, dtype=float)
+    T = np.asarray(grid.init_temperatures, dtype=float)
+    vals = np.broadcast_to(row, (p.size, T.size, lam.size))
+    return {"1H2-16O": OpacityTable(vals, p, T, lam).drop_duplicates("temperature")}
+
+
+def binned_opacity(*args, **kwargs):
+    """Binning of high-resolution DACE cross-sections (opacity.py:66-170) is the next
+    component of SURVEY.md §8(f) and not part of this round's engine."""
+    raise NotImplementedError("binned_opacity: pass precomputed tables via "
+                              "Grid.load_opacities(opacities=...) (SURVEY.md §8(f) #1)")

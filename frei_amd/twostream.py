@@ -1,0 +1,103 @@
+"""Two-stream flux propagation, emit and absorb (frei/twostream.py), on the GPU.
+
+Same names, arguments and tuple returns as the reference; ``fluxes_up``/``fluxes_down``
+passed by the caller are updated in place and returned (twostream.py:290-294, 418-421).
+Units: wavelength µm, temperature K, pressure bar, flux erg s^-1 cm^-3, g cm s^-2,
+m_bar g (astropy Quantities are accepted and converted when astropy is installed).
+"""
+import numpy as np
+
+from .constants import C, H, K_B, M_BAR_DEFAULT, UM
+from .engine import ABSORB, EMIT, Engine, propagate_fluxes_device
+from .units import scalar, value
+
+__all__ = ["propagate_fluxes", "emit", "absorb", "BB", "E"]
+
+
+def BB(temperature):
+    """Planck function factory (twostream.py:46-67): BB(T)(lam [µm]) -> erg s^-1 cm^-3 sr^-1."""
+    T = scalar(temperature, "K")
+
+    def planck(wavelength):
+        lam_cm = value(wavelength, "um") * UM
+        return 2 * H * C ** 2 / np.power(lam_cm, 5) / np.expm1(H * C / (lam_cm * K_B * T))
+    return planck
+
+
+def E(omega_0, g_0):
+    """Deitrick 2020 Eqn 19 correction (twostream.py:70-94)."""
+    return np.where(omega_0 > 0.1,
+                    1.225 - 0.1582 * g_0 - 0.1777 * omega_0 - 0.07465 * g_0 ** 2
+                    + 0.2351 * omega_0 * g_0 - 0.05582 * omega_0 ** 2, 1)
+
+
+def propagate_fluxes(lam, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0=0, g_0=0, eps=0.5,
+                     device=0):
+    """Improved two-stream update of one layer pair, elementwise over wavelength
+    (twostream.py:97-177) -> (F_2_up, F_1_down).  The engine implements the g_0 = 0
+    case every call site uses (twostream.py:389, 518); ``eps`` is unused as in the
+    reference."""
+    if np.any(np.asarray(g_0) != 0):
+        raise ValueError("propagate_fluxes: only g_0 = 0 is implemented (as used by emit/absorb)")
+    flux = "erg / (s cm3)"
+    return propagate_fluxes_device(value(lam, "um"), value(F_1_up, flux), value(F_2_down, flux),
+                                   scalar(T_1, "K"), scalar(T_2, "K"),
+                                   np.asarray(delta_tau, dtype=float),
+                                   np.asarray(omega_0, dtype=float), device=device)
+
+
+def _sweeps(direction, opacities, temperatures, pressures, lam, F_TOA, g, m_bar, n_timesteps,
+            convergence_thresh, alpha, fluxes_up, fluxes_down, device):
+    T = np.array(value(temperatures, "K"), dtype=float)
+    p = value(pressures, "bar")
+    lam_um = value(lam, "um")
+    nL, nlam = p.size, lam_um.size
+    ftoa = np.asarray(value(F_TOA, "erg / (s cm3)"), dtype=float)
+    eng = Engine(lam_um, p, opacities, g=g, m_bar=m_bar, F_toa=ftoa, device=device)
+    try:
+        up_in, down_in = fluxes_up, fluxes_down
+        up = np.zeros((nL, nlam)) if up_in is None else np.array(value(up_in, "erg / (s cm3)"))
+        down = (np.zeros((nL, nlam)) if down_in is None
+                else np.array(value(down_in, "erg / (s cm3)")))
+        if up_in is None and direction == ABSORB:
+            up[0] = np.pi * BB(T[0])(lam_um)          # twostream.py:468-470 (Q5)
+        if down_in is None:
+            down[-1] = ftoa                            # twostream.py:337-339, 472-474
+        eng.set_fluxes(up, down)
+        hist = np.zeros((nL, n_timesteps + 1))
+        hist[:, 0] = T
+        dtaus = dT = None
+        for j in range(n_timesteps):
+            eng.set_temperatures(hist[:, j])
+            dT, _, dtaus = eng.sweep(direction, alpha=alpha)
+            hist[:, j + 1] = hist[:, j] - dT
+            if n_timesteps > 1 and np.abs(dT).max() < convergence_thresh:
+                break
+        up, down = eng.get_fluxes()
+    finally:
+        eng.close()
+    # the reference mutates the caller's arrays in place
+    if isinstance(up_in, np.ndarray) and up_in.dtype == np.float64:
+        up_in[...] = up
+        up = up_in
+    if isinstance(down_in, np.ndarray) and down_in.dtype == np.float64:
+        down_in[...] = down
+        down = down_in
+    return up, down, hist[:, j + 1].copy(), hist, dtaus, dT
+
+
+def emit(opacities, temperatures, pressures, lam, F_TOA, g, m_bar=M_BAR_DEFAULT,
+         n_timesteps=50, convergence_thresh=10.0, alpha=1, fluxes_up=None, fluxes_down=None,
+         device=0):
+    """Upward sweep(s) (twostream.py:290-421) ->
+    (fluxes_up, fluxes_down, final_temps, temperature_history, dtaus, dT)."""
+    return _sweeps(EMIT, opacities, temperatures, pressures, lam, F_TOA, g, m_bar, n_timesteps,
+                   convergence_thresh, alpha, fluxes_up, fluxes_down, device)
+
+
+def absorb(opacities, temperatures, pressures, lam, F_TOA, g, m_bar=M_BAR_DEFAULT,
+           n_timesteps=50, convergence_thresh=10.0, alpha=1, fluxes_up=None, fluxes_down=None,
+           device=0):
+    """Downward sweep(s) (twostream.py:424-550), same returns as :func:`emit`."""
+    return _sweeps(ABSORB, opacities, temperatures, pressures, lam, F_TOA, g, m_bar,
+                   n_timesteps, convergence_thresh, alpha, fluxes_up, fluxes_down, device)

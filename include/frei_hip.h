@@ -1,0 +1,149 @@
+/*
+ * frei_hip.h — C ABI of the MI355X (gfx950) two-stream radiative-transfer engine.
+ *
+ * Drop-in boundary for bmorris3/frei's hot path.  The reference
+ * has no FFI: its seam is a set of Python functions, and each entry point below
+ * replaces one of them (file:line in /root/reference):
+ *
+ *   frei_propagate_fluxes   frei/twostream.py:97-177   propagate_fluxes(...)
+ *   frei_kappa              frei/opacity.py:203-269    kappa(opacities, T, p, lam, m_bar)
+ *   frei_sweep              frei/twostream.py:290-421  emit(..., n_timesteps=1)
+ *                           frei/twostream.py:424-550  absorb(..., n_timesteps=1)
+ *   frei_run                frei/core.py:233-338       Grid.emission_spectrum(...)
+ *   frei_set_table*         frei/core.py:198-231       Grid.load_opacities(opacities=...)
+ *   frei_set_grid           frei/core.py:113-188,48-55 Grid(...) + F_TOA(...)
+ *
+ * Conventions (all plain pointers and sizes, no framework types):
+ *   - Units are cgs: wavelength cm, pressure dyn cm^-2, T K, flux erg s^-1 cm^-3,
+ *     opacity cm^2 g^-1, g cm s^-2, masses g.  Layer index 0 = bottom of atmosphere.
+ *   - Every function returns 0 on success, < 0 on error; frei_last_error() then holds
+ *     a message (thread-local).  The Python layer raises RuntimeError with it.
+ *   - Host buffers are caller-owned and copied in/out; device buffers belong to the
+ *     context.  One context per GPU; a context is not thread-safe.
+ *   - A context owns the contiguous wavelength slice [lam_offset, lam_offset+n_lam)
+ *     of a global grid; with nranks > 1 the per-sweep bolometric partial sums are
+ *     all-gathered over RCCL (frei_comm_init) and summed in rank order, so every rank
+ *     computes bitwise-identical temperatures.
+ */
+#ifndef FREI_HIP_H
+#define FREI_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct frei_ctx frei_ctx;
+
+enum { FREI_EMIT = 0, FREI_ABSORB = 1 };
+
+/* Library/ABI version (major*10000 + minor*100 + patch). */
+int frei_version(void);
+/* Message of the last failing call on this thread ("" if none). */
+const char* frei_last_error(void);
+/* Number of visible HIP devices. */
+int frei_device_count(int* n);
+
+/* Context for n_layers x n_lam (local slice) x n_species on `device`. */
+int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int n_species);
+int frei_ctx_destroy(frei_ctx* ctx);
+
+/*
+ * Grid and per-wavelength constants (frei/core.py:113-188, 48-55; twostream.py:46-67).
+ *   c1[n_lam]     2 h c^2 / lam^5                (Planck prefactor, BB)
+ *   lk[n_lam]     lam * k_B                      (BB exponent is h c / (lk * T))
+ *   sigma[n_lam]  Rayleigh H2 + He, cm^2 g^-1    (opacity.py:173-200, 233)
+ *   f_toa[n_lam]  stellar flux at TOA            (core.py:48-55)
+ *   trapz_w[n_lam] per-point trapezoid weights of the GLOBAL grid (cm), sliced
+ *   p[n_layers]   layer pressures, dyn cm^-2, descending (tp.py:10-33)
+ *   g, m_bar      planet gravity and mean molecular mass (core.py:65-106)
+ */
+int frei_set_grid(frei_ctx* ctx, const double* c1, const double* lk, const double* sigma,
+                  const double* f_toa, const double* trapz_w, const double* p,
+                  double g, double m_bar);
+
+/*
+ * Opacity table of species s (Grid.load_opacities(opacities=...), core.py:198-231):
+ * values[n_p][n_T][n_lam] (row-major, this context's wavelength slice), cm^2 g^-1,
+ * on nodes p_nodes[n_p] (dyn cm^-2) x T_nodes[n_T] (K), any order.  Linear
+ * interpolation with fill 0 outside the node hull (opacity.py:241-263); a table with
+ * one unique T is interpolated in pressure only (opacity.py:256-259).
+ */
+int frei_set_table(frei_ctx* ctx, int s, const double* values, const double* p_nodes, int n_p,
+                   const double* T_nodes, int n_T);
+/*
+ * Same, but the table is generated on the device (no host copy of n_p*n_T*n_lam values):
+ * values[p][t][l] = min(max((fp[p] * fT[t]) * base[l], lo), hi).  Synthetic separable
+ * tables for benchmarks and parity tests.
+ */
+int frei_set_table_separable(frei_ctx* ctx, int s, const double* base, const double* fp,
+                             const double* fT, double lo, double hi, const double* p_nodes,
+                             int n_p, const double* T_nodes, int n_T);
+/* Per-species, per-layer mass mixing ratios mmr[n_species][n_layers] (chemistry.py:114-205;
+ * the reference's mock gives a constant VMR).  CIA-like tables take their weights here. */
+int frei_set_mmr(frei_ctx* ctx, const double* mmr);
+
+/* Flux state [n_layers][n_lam] (this slice), caller layout row-major. */
+int frei_set_fluxes(frei_ctx* ctx, const double* up, const double* down);
+int frei_get_fluxes(frei_ctx* ctx, double* up, double* down);
+int frei_set_temperatures(frei_ctx* ctx, const double* T);
+int frei_get_temperatures(frei_ctx* ctx, double* T);
+
+/*
+ * One sweep with the current temperatures (emit: twostream.py:351-407, absorb: 486-536),
+ * in place on the flux state, then T <- T - dT (Q11).  alpha = mixing-length parameter.
+ * Optional outputs (NULL to skip): dT[n_layers], bol[n_layers][4] = bolometric
+ * (F_2_up, F_2_down, F_1_up, F_1_down) per sweep step, dtaus[n_layers][n_lam] (row 0 = 1,
+ * row k = k-th step of the sweep, Q12).
+ */
+int frei_sweep(frei_ctx* ctx, int direction, double alpha, double* dT, double* bol,
+               double* dtaus);
+
+/*
+ * Grid.emission_spectrum (core.py:233-338): zero fluxes, T = T_init, up to n_timesteps
+ * (emit, absorb) iterations with the reference convergence test (sign flips of the
+ * absorb temperature history > n_zero_crossings, or |dT| < convergence_dT, for all
+ * layers), then a final emit with alpha = 1.  The loop stays on the device; the host
+ * polls the convergence flag once per chunk of iterations.
+ * Outputs: *n_iter; T_final[n_layers]; temp_hist[n_layers][2*n_iter] (may be NULL; caller
+ * sizes it for n_timesteps); dtaus[n_layers][n_lam] (may be NULL); spectrum[n_lam]
+ * = F_up[n_layers-1] (may be NULL).
+ */
+int frei_run(frei_ctx* ctx, const double* T_init, int n_timesteps, int n_zero_crossings,
+             double convergence_dT, double alpha, int* n_iter, double* T_final,
+             double* temp_hist, double* dtaus, double* spectrum);
+
+/* Benchmark/driver pieces of frei_run (all asynchronous on the context's stream). */
+int frei_state_init(frei_ctx* ctx, const double* T_init);
+/* n T-P iterations; convergence is tracked but never stops the work when
+ * n_zero_crossings < 0 (fixed-work benchmark steps). */
+int frei_iterate(frei_ctx* ctx, int n, int n_zero_crossings, double convergence_dT,
+                 double alpha);
+int frei_synchronize(frei_ctx* ctx);
+
+/* kappa (opacity.py:203-269) at one (T, p) on this slice: k[n_lam] (includes sigma, Q1),
+ * sigma[n_lam] (may be NULL). */
+int frei_kappa(frei_ctx* ctx, double T, double p, double* k, double* sigma);
+
+/* propagate_fluxes (twostream.py:97-177), elementwise on n points, g_0 = 0. */
+int frei_propagate_fluxes(int device, int64_t n, const double* c1, const double* lk,
+                          const double* F_1_up, const double* F_2_down, double T_1,
+                          double T_2, const double* delta_tau, const double* omega_0,
+                          double* F_2_up, double* F_1_down);
+
+/* Multi-GPU: 128-byte RCCL unique id (rank 0 creates, others receive it out of band),
+ * then every rank joins.  Per sweep: one ncclAllGather of n_layers*4 doubles. */
+int frei_comm_unique_id(void* id128);
+int frei_comm_init(frei_ctx* ctx, int nranks, int rank, const void* id128);
+
+/* Timing of the sweep kernel (HIP events on the context stream around every sweep
+ * launch while enabled): total milliseconds and number of timed launches. */
+int frei_timing_enable(frei_ctx* ctx, int on);
+int frei_timing_read(frei_ctx* ctx, double* total_ms, int* n_launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FREI_HIP_H */

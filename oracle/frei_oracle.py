@@ -187,7 +187,8 @@ class Table:
     """(pressure [bar], temperature [K], wavelength) grid, like the reference's DataArray."""
 
     def __init__(self, values, pressure, temperature, wavelength=None):
-        self.values = np.asarray(values, dtype=float)
+        self.values = values if hasattr(values, "shape") and not isinstance(values, list) \
+            and not isinstance(values, np.ndarray) else np.asarray(values, dtype=float)
         self.pressure = np.asarray(pressure, dtype=float)
         self.temperature = np.asarray(temperature, dtype=float)
         self.wavelength = wavelength
@@ -466,3 +467,18 @@ def example_opacity(p_bar, T_nodes, lam_um, seed=42, scale_factor=20):
 def separable_table(base, fp, fT, lo=1e-4, hi=1e3):
     """Synthetic separable table used by the goldens/bench: clip(fp[p]*fT[T]*base[lam])."""
     return np.clip((fp[:, None] * fT[None, :])[:, :, None] * base[None, None, :], lo, hi)
+
+
+class SeparableValues:
+    """Lazy (n_p, n_T, n_lam) view of separable_table(base, fp, fT): rows are built on
+    indexing, so the CPU baseline can run large grids without materialising the table."""
+
+    def __init__(self, base, fp, fT, lo=1e-4, hi=1e3):
+        self.base, self.fp, self.fT = (np.asarray(a, dtype=float) for a in (base, fp, fT))
+        self.lo, self.hi = lo, hi
+        self.shape = (self.fp.size, self.fT.size, self.base.size)
+
+    def __getitem__(self, pidx):
+        fp = self.fp[pidx]
+        return np.clip((fp[:, None] * self.fT[None, :])[:, :, None] * self.base[None, None, :],
+                       self.lo, self.hi)

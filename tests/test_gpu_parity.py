@@ -1,0 +1,216 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden vectors
+and the CPU oracle.  Criterion (tests/parity.py): |x - ref| <= 1e-10 |ref| + 4 delta cond,
+cond = the oracle's first-order condition array of the reference formula."""
+import numpy as np
+import pytest
+
+from oracle import frei_oracle as O
+from tests.parity import EPS, assert_flux_parity, rel, row_normwise
+
+pytestmark = pytest.mark.gpu
+
+G_J, M_BAR = 2478.6519476149147, 4.0142926168559996e-24
+
+
+@pytest.fixture(scope="module")
+def fa():
+    import frei_amd
+    from frei_amd import _native as N
+    assert N.device_count() >= 1, "no HIP device visible"
+    return frei_amd
+
+
+def _cond(shape):
+    return dict(up=np.zeros(shape), down=np.zeros(shape), delta=1.0)
+
+
+def test_propagate_fluxes_matches_reference(fa, golden):
+    P = golden("propagate.npz")
+    for c in range(int(P["n_cases"])):
+        args = (P["lam"] * 1e-4, P[f"c{c}_F1u"], P[f"c{c}_F2d"], float(P[f"c{c}_T1"]),
+                float(P[f"c{c}_T2"]), P[f"c{c}_dtau"], P[f"c{c}_omega"])
+        F2u, F1d = fa.propagate_fluxes(P["lam"], P[f"c{c}_F1u"], P[f"c{c}_F2d"], args[3],
+                                       args[4], P[f"c{c}_dtau"], P[f"c{c}_omega"])
+        cu, cd = O.propagate_error_bound(*args, delta=1.0)
+        assert_flux_parity(F2u, P[f"c{c}_F2u"], cu, what=f"case{c} F_2_up vs reference")
+        assert_flux_parity(F1d, P[f"c{c}_F1d"], cd, what=f"case{c} F_1_down vs reference")
+        o2u, o1d = O.propagate_fluxes(*args)
+        assert_flux_parity(F2u, o2u, cu, what=f"case{c} F_2_up vs oracle")
+        assert_flux_parity(F1d, o1d, cd, what=f"case{c} F_1_down vs oracle")
+
+
+def test_propagate_fluxes_rejects_nonzero_g0(fa):
+    with pytest.raises(ValueError):
+        fa.propagate_fluxes([1.0, 2.0], [1, 1], [1, 1], 1000, 900, [1, 1], [0, 0], g_0=0.5)
+
+
+def test_kappa_matches_reference(fa, golden):
+    s = golden("setup_c1.npz")
+    K = golden("kappa.npz")
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), T_ref=2400)
+    op = fa.load_example_opacity(grid, scale_factor=1)
+    for j in range(len(K["ex_T"])):
+        k, sig = fa.kappa(op, K["ex_T"][j], K["ex_p"][j], s["lam"], m_bar=M_BAR)
+        assert rel(k, K["ex_k"][j]) < 1e-13, j
+        assert rel(sig, K["ex_sigma"][j]) < 1e-13
+    tabs2 = {n: fa.OpacityTable(O.separable_table(K[f"sep{i}_base"], K[f"sep{i}_fp"],
+                                                  K[f"sep{i}_fT"]), K["sep_p"], K["sep_Tnodes"])
+             for i, n in enumerate(["1H2-16O", "12C-16O"])}
+    for j in range(len(K["sep_T"])):
+        k, _ = fa.kappa(tabs2, K["sep_T"][j], K["sep_pq"][j], K["sep_lam"], m_bar=M_BAR)
+        assert rel(k, K["sep_k"][j]) < 1e-13, j
+    one = {"1H2-16O": fa.OpacityTable(
+        np.clip(K["oneT_fp"][:, None, None] * K["oneT_base"][None, None, :], 1e-4, 1e3),
+        K["sep_p"], [1234.0])}
+    for j in range(len(K["oneT_T"])):
+        k, _ = fa.kappa(one, K["oneT_T"][j], K["oneT_p"][j], K["sep_lam"], m_bar=M_BAR)
+        assert rel(k, K["oneT_k"][j]) < 1e-13, j
+
+
+@pytest.mark.parametrize("kind", ["emit", "absorb"])
+def test_standalone_sweep_matches_reference(fa, golden, kind):
+    s = golden("setup_c1.npz")
+    EA = golden("emit_absorb_c1.npz")
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), T_ref=2400)
+    op = fa.load_example_opacity(grid, scale_factor=1)
+    fn = fa.emit if kind == "emit" else fa.absorb
+    fu, fd, T, th, dtaus, dT = fn(op, grid.init_temperatures, grid.pressures, grid.lam,
+                                  s["F_TOA"], G_J, m_bar=M_BAR, n_timesteps=1)
+    tabs = O.example_opacity(s["pressures"], s["init_temperatures"], s["lam"], scale_factor=1)
+    cond = _cond((30, 500))
+    ofn = O.emit if kind == "emit" else O.absorb
+    ofn(tabs, s["init_temperatures"], s["pressures"], s["lam"], s["F_TOA"], G_J, M_BAR, 1,
+        err=cond)
+    assert_flux_parity(fu, EA[kind + "_F_up"], cond["up"], what=kind + " F_up")
+    assert_flux_parity(fd, EA[kind + "_F_down"], cond["down"], what=kind + " F_down")
+    assert rel(T, EA[kind + "_T"]) < 1e-12
+    assert np.max(np.abs(dT - EA[kind + "_dT"])) < 1e-8
+    assert row_normwise(dtaus, EA[kind + "_dtaus"]) < 1e-13
+
+
+def test_single_sweep_from_identical_state_matches_oracle(fa):
+    """Strict single-sweep check (delta = eps) from a non-trivial state, 2 species."""
+    rng = np.random.default_rng(3)
+    lam, _, _ = O.wavelength_grid(0.5, 10, 1024)
+    p = O.pressure_grid(24, -6, np.log10(200))
+    T = O.temperature_grid(p, 1800.0, 0.1, 0.1) * (1 + 0.05 * rng.standard_normal(24))
+    Tn = np.linspace(0.7 * T.min(), 1.3 * T.max(), 7)
+    names = ["1H2-16O", "12C-16O"]
+    tabs_o, tabs_f = {}, {}
+    for i, n in enumerate(names):
+        base = 10 ** rng.uniform(-2, 2, lam.size)
+        fp, fT = (p / 1.0) ** 0.1, (Tn / 1000) ** 0.5
+        v = O.separable_table(base, fp, fT)
+        tabs_o[n] = O.Table(v, p, Tn)
+        tabs_f[n] = fa.OpacityTable(v, p, Tn)
+    up0 = 10 ** rng.uniform(8, 12, (24, lam.size))
+    down0 = 10 ** rng.uniform(6, 11, (24, lam.size))
+    Ft = O.F_TOA(lam)
+    for kind in ("emit", "absorb"):
+        cond = _cond((24, lam.size))
+        ofn = O.emit if kind == "emit" else O.absorb
+        ou, od, oT, odt, odT = ofn(tabs_o, T, p, lam, Ft, G_J, M_BAR, 1, up0.copy(),
+                                   down0.copy(), err=cond)
+        fn = fa.emit if kind == "emit" else fa.absorb
+        up, down = up0.copy(), down0.copy()
+        fu, fd, fT_, _, fdt, fdT = fn(tabs_f, T, p, lam, Ft, G_J, m_bar=M_BAR, n_timesteps=1,
+                                      fluxes_up=up, fluxes_down=down)
+        assert fu is up and fd is down            # in-place update like the reference
+        assert_flux_parity(fu, ou, cond["up"], EPS, kind + " F_up")
+        assert_flux_parity(fd, od, cond["down"], EPS, kind + " F_down")
+        assert rel(fT_, oT) < 1e-12
+        assert row_normwise(fdt, odt) < 1e-14
+
+
+def _grid_run(fa, C, pre, tabs_f, tabs_o, lam, p, T0, n, Ft=None):
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), lam=lam, pressures=p, init_temperatures=T0)
+    grid.load_opacities(opacities=tabs_f)
+    spec, T, th, dtaus = grid.emission_spectrum(n_timesteps=n)
+    cond = _cond((len(p), len(lam)))
+    O.emission_spectrum(tabs_o, T0, p, lam, O.F_TOA(lam) if Ft is None else Ft, G_J, M_BAR,
+                        1, n_timesteps=n, err=cond)
+    relT = rel(T, C[pre + "final_T"])
+    assert relT < 1e-10, relT
+    delta = max(EPS, relT)
+    assert_flux_parity(spec.flux, C[pre + "spectrum"], cond["up"][-1], delta, pre + "spectrum")
+    assert rel(th, C[pre + "temp_hist"]) < 1e-10
+    assert th.shape == C[pre + "temp_hist"].shape
+    assert row_normwise(dtaus, C[pre + "dtaus"]) < 1e-10
+    up, down = grid.engine().get_fluxes()
+    assert_flux_parity(up, C[pre + "F_up"], cond["up"], delta, pre + "F_up")
+    assert_flux_parity(down, C[pre + "F_down"], cond["down"], delta, pre + "F_down")
+    return grid, spec, T, dtaus
+
+
+def test_c1_emission_spectrum_matches_reference(fa, golden):
+    s = golden("setup_c1.npz")
+    C = golden("c1_step1.npz")
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), T_ref=2400)
+    tabs_f = fa.load_example_opacity(grid, scale_factor=1)
+    tabs_o = O.example_opacity(s["pressures"], s["init_temperatures"], s["lam"], scale_factor=1)
+    g, spec, T, dtaus = _grid_run(fa, C, "ex_", tabs_f, tabs_o, s["lam"], s["pressures"],
+                                  s["init_temperatures"], 1)
+    assert rel(spec.flux, C["ex_spectrum"]) < 1e-10    # emergent spectrum, elementwise
+    teff = fa.effective_temperature(g, spec, dtaus, T)
+    assert abs(teff - float(C["ex_Teff"])) < 1e-6
+    gray_o = {"1H2-16O": O.Table(np.ones((30, 30, 500)), s["pressures"], s["init_temperatures"])}
+    gray_f = {"1H2-16O": fa.OpacityTable(np.ones((30, 30, 500)), s["pressures"],
+                                         s["init_temperatures"])}
+    _grid_run(fa, C, "gray_", gray_f, gray_o, s["lam"], s["pressures"], s["init_temperatures"], 1)
+
+
+def test_c1_converges_in_50_iterations_like_reference(fa, golden):
+    s = golden("setup_c1.npz")
+    C = golden("c1_converge.npz")
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), T_ref=2400)
+    tabs_f = fa.load_example_opacity(grid, scale_factor=1)
+    tabs_o = O.example_opacity(s["pressures"], s["init_temperatures"], s["lam"], scale_factor=1)
+    _, spec, T, _ = _grid_run(fa, C, "cv_", tabs_f, tabs_o, s["lam"], s["pressures"],
+                              s["init_temperatures"], 100)
+    assert rel(spec.flux, C["cv_spectrum"]) < 1e-10
+
+
+def test_c2small_two_species_matches_reference(fa, golden):
+    C = golden("c2small.npz")
+    names = ["1H2-16O", "12C-16O"]
+    tabs_o = {n: O.Table(O.separable_table(C[f"s{i}_base"], C[f"s{i}_fp"], C[f"s{i}_fT"]),
+                         C["pressures"], C["T_nodes"]) for i, n in enumerate(names)}
+    tabs_f = {n: fa.SeparableTable(C[f"s{i}_base"], C[f"s{i}_fp"], C[f"s{i}_fT"],
+                                   C["pressures"], C["T_nodes"]) for i, n in enumerate(names)}
+    _grid_run(fa, C, "", tabs_f, tabs_o, C["lam"], C["pressures"], C["init_temperatures"], 3)
+
+
+def test_eight_species_device_tables_match_oracle(fa):
+    """C3-like: 8 species (6 molecules + 2 CIA-style tables with supplied weights),
+    device-generated separable tables, 60 layers x 4096, two T-P iterations."""
+    rng = np.random.default_rng(11)
+    lam, _, _ = O.wavelength_grid(0.5, 10, 4096)
+    p = O.pressure_grid(60, -6, np.log10(200))
+    T0 = O.temperature_grid(p, 1500.0, 0.1, 0.1)
+    Tn = np.linspace(0.8 * T0.min(), 1.2 * T0.max(), 16)
+    names = ["1H2-16O", "12C-16O", "12C-16O2", "12C-1H4", "Na", "K", "H2-H2", "H2-He"]
+    mmr = np.vstack([O.mock_mmr(names[:6], M_BAR)[:, None] * np.ones(60),
+                     1e-3 * (p / p[0]) ** 0.5, 5e-4 * np.ones(60)])
+    tabs_o, tabs_f = {}, {}
+    for i, n in enumerate(names):
+        base = 10 ** (rng.uniform(-3, 1, lam.size))
+        fp, fT = (p / 1.0) ** 0.1, (Tn / 1000.0) ** 0.5
+        tabs_o[n] = O.Table(O.separable_table(base, fp, fT), p, Tn)
+        tabs_f[n] = fa.SeparableTable(base, fp, fT, p, Tn)
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), lam=lam, pressures=p, init_temperatures=T0)
+    grid.load_opacities(opacities=tabs_f, mmr=mmr)
+    spec, T, th, dtaus = grid.emission_spectrum(n_timesteps=2, n_zero_crossings=10**6,
+                                                convergence_dT=-1)
+    cond = _cond((60, lam.size))
+    osp, oT, oth, odt, ou, od, it = O.emission_spectrum(
+        tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1, n_timesteps=2,
+        n_zero_crossings=10**6, convergence_dT=-1, mmr=mmr, err=cond)
+    relT = rel(T, oT)
+    assert relT < 1e-10
+    assert th.shape == (60, 4)
+    delta = max(EPS, relT)
+    assert_flux_parity(spec.flux, osp, cond["up"][-1], delta, "spectrum")
+    up, down = grid.engine().get_fluxes()
+    assert_flux_parity(up, ou, cond["up"], delta, "F_up")
+    assert_flux_parity(down, od, cond["down"], delta, "F_down")
+    assert row_normwise(dtaus, odt) < 1e-10
