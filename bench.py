@@ -117,7 +117,7 @@ def main():
             N.check(N.lib().frei_comm_unique_id(buf))
             uid = buf.raw
         uid = d.bcast_bytes(uid)
-        comm = (d.world, d.rank, uid)
+        comm = ("rccl", d.world, d.rank, uid)
     tabs = {n: SeparableTable(w["base"][s], w["fp"][s], w["fT"][s], w["p"], w["T_nodes"])
             for s, n in enumerate(w["names"])}
     eng = Engine(w["lam"], w["p"], tabs, mmr=w["mmr"], device=d.local, lam_slice=(lo, hi),

@@ -17,6 +17,9 @@ _ip = ctypes.POINTER(ctypes.c_int)
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
 
+# int (*)(const double* send, double* recv, int64_t n, void* user)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, _dp, _dp, _i64, _vp)
+
 # name -> (restype, argtypes); mirrors include/frei_hip.h exactly
 SIGNATURES = {
     "frei_version": (ctypes.c_int, []),
@@ -50,6 +53,8 @@ SIGNATURES = {
                                              _dp]),
     "frei_comm_unique_id": (ctypes.c_int, [_vp]),
     "frei_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp]),
+    "frei_comm_init_host": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
+                                           "ALLGATHER_FN", _vp]),
     "frei_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "frei_timing_read": (ctypes.c_int, [_vp, _dp, _ip]),
 }
@@ -68,7 +73,7 @@ def lib():
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res
-            fn.argtypes = args
+            fn.argtypes = [ALLGATHER_FN if a == "ALLGATHER_FN" else a for a in args]
         _lib = L
     return _lib
 

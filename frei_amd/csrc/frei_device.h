@@ -36,6 +36,16 @@ struct StepP {
   int64_t pad;
 };
 
+// Fast-path sweep step (every species: on-node pressure, >= 2 T nodes, S <= kMaxFastS):
+// two T-bracket rows per species, row_hi = row_lo + n_lam (T axis stored ascending).
+constexpr int kMaxFastS = 8;
+struct FastStep {
+  double T1, T2, dm;
+  int32_t layer, top;
+  double wlo[kMaxFastS], whi[kMaxFastS], mmr[kMaxFastS];
+  int64_t off[kMaxFastS];  // element offset of the T_lo row in species s's table
+};
+
 // Interpolation term of one species at one layer (opacity.py:250-263).
 struct TermP {
   const double* row[4];  // table rows (device pointers), corner order of scipy interpn
@@ -139,6 +149,20 @@ struct SetupArgs {
   const double* mmr;       // [n_species][n_layers]
   StepP* steps;            // [n_layers - 1]
   TermP* terms;            // [n_layers - 1][n_species]
+  FastStep* fsteps;        // [n_layers - 1] (fast path)
+};
+
+struct FastArgs {
+  int64_t n_lam;
+  int n_steps, force;
+  const double *c1, *lk, *sig, *wtr, *ftoa;
+  const double* tab[kMaxFastS];
+  const FastStep* steps;
+  double* F_up;
+  double* F_down;
+  double* dtaus;
+  double* part;
+  const int* conv;
 };
 
 struct SweepArgs {
@@ -169,6 +193,7 @@ struct UpdateArgs {
 
 // launchers (frei_kernels.hip)
 void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st);
+void launch_sweep_fast(int dir, int S, const FastArgs& a, int nblocks, hipStream_t st);
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
                    int force, hipStream_t st);
 void launch_setup(const SetupArgs& u, int dir, hipStream_t st);

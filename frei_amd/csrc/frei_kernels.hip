@@ -90,6 +90,24 @@ __device__ __forceinline__ double kappa_at(const TermP* __restrict__ t, int nS, 
   return tot + sig;  // k includes sigma (Q1)
 }
 
+// Sum four per-lane values over the wave64 with 7 exchanges (instead of 4 x 6): after the
+// first two butterfly levels each lane carries one of the four partial sums.  Lane 0 ends
+// with sum(q0), lane 2 with sum(q1), lane 1 with sum(q2), lane 3 with sum(q3).  Fixed order
+// (commutative pairs), so the result is deterministic.
+__device__ __forceinline__ double wave_sum4(double q0, double q1, double q2, double q3,
+                                            int lane) {
+  const bool odd = lane & 1;
+  const double r0 = __shfl_xor(odd ? q0 : q2, 1, 64);
+  const double r1 = __shfl_xor(odd ? q1 : q3, 1, 64);
+  const double x0 = (odd ? q2 : q0) + r0;
+  const double x1 = (odd ? q3 : q1) + r1;
+  const bool b1 = lane & 2;
+  double y = (b1 ? x1 : x0) + __shfl_xor(b1 ? x0 : x1, 2, 64);
+#pragma unroll
+  for (int o = 4; o <= 32; o <<= 1) y += __shfl_xor(y, o, 64);
+  return y;
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -151,14 +169,8 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
       Fd[(int64_t)i * nl + j] = F1d;
       if (a.dtaus) a.dtaus[(int64_t)(k + 1) * nl + j] = dtau;
     }
-    const double q0 = wave_sum(wt * F2u);
-    const double q1 = wave_sum(wt * F2d);
-    const double q2 = wave_sum(wt * F1u);
-    const double q3 = wave_sum(wt * F1d);
-    if (lane == 0) {
-      double* r = red + ((int64_t)wv * ns + k) * 4;
-      r[0] = q0; r[1] = q1; r[2] = q2; r[3] = q3;
-    }
+    const double y = wave_sum4(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
+    if (lane < 4) red[((int64_t)wv * ns + k) * 4 + (lane & 1) * 2 + ((lane >> 1) & 1)] = y;
     if (DIR == kEmit) { carry = F2u; Bc = B2; } else { carry = F1d; Bc = B1; }
   }
   __syncthreads();
@@ -167,6 +179,99 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     double v = red[idx];
     for (int w = 1; w < nw; ++w) v += red[(int64_t)w * ns * 4 + idx];
     a.part[(int64_t)idx * gridDim.x + blockIdx.x] = v;
+  }
+}
+
+// ---------------------------------------------------------------- K1 fast path
+// Software-pipelined: the next step's 2S table rows and its stale opposite-stream flux
+// are loaded into registers while the current step computes, so HBM latency overlaps the
+// fp64 two-stream arithmetic instead of serialising with it.
+template <int DIR, int S>
+__global__ __launch_bounds__(kBlock) void sweep_fast_kernel(
+    FastArgs a, const FastStep* __restrict__ st, double* __restrict__ Fu,
+    double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
+  if (!a.force && *a.conv) return;
+  extern __shared__ double red[];  // [wave][step][4]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int64_t nl = a.n_lam;
+  const int64_t j0 = (int64_t)blockIdx.x * kBlock + tid;
+  const bool act = j0 < nl;
+  const int64_t j = act ? j0 : nl - 1;
+  const double c1 = a.c1[j], lk = a.lk[j], sig = a.sig[j];
+  const double wt = act ? a.wtr[j] : 0.0;
+  const int ns = a.n_steps;
+
+  double v[2 * S];
+  double stale;
+  auto prefetch = [&](int k) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double* r = a.tab[s] + st[k].off[s] + j;
+      v[2 * s] = __builtin_nontemporal_load(r);
+      v[2 * s + 1] = __builtin_nontemporal_load(r + nl);
+    }
+    const int i = st[k].layer;
+    const double* src = (DIR == kEmit) ? (st[k].top ? a.ftoa : Fd + (int64_t)(i + 1) * nl)
+                                       : Fu + (int64_t)i * nl;
+    stale = src[j];
+  };
+  prefetch(0);
+  double carry, Bc;
+  if (DIR == kEmit) {
+    carry = Fu[(int64_t)st[0].layer * nl + j];
+    Bc = planck(c1, lk, st[0].T1);
+  } else {
+    carry = Fd[(int64_t)(st[0].layer + 1) * nl + j];
+    Bc = planck(c1, lk, st[0].T2);
+  }
+  for (int k = 0; k < ns; ++k) {
+    const int i = st[k].layer;
+    const int top = st[k].top;
+    const double T1 = st[k].T1, T2 = st[k].T2, dm = st[k].dm;
+    double tot = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double acc = (0.0 + v[2 * s] * st[k].wlo[s]) + v[2 * s + 1] * st[k].whi[s];
+      double ops = st[k].mmr[s] * acc;
+      if (S > 1) ops = isnan(ops) ? 0.0 : ops;  // xarray nansum for S > 1 (Q8)
+      tot = (s == 0) ? ops : tot + ops;
+    }
+    const double F_st = stale;
+    prefetch(k + 1 < ns ? k + 1 : k);  // unconditional: keeps vmcnt waits counted
+    const double kap = tot + sig;
+    const double dtau = dm * kap;
+    const double w0 = sig / (sig + kap);
+    double B1, B2, F1u, F2d;
+    if (DIR == kEmit) {
+      B1 = Bc;
+      B2 = top ? Bc : planck(c1, lk, T2);
+      F1u = carry;
+      F2d = F_st;
+    } else {
+      B2 = Bc;
+      B1 = planck(c1, lk, T1);
+      F2d = carry;
+      F1u = F_st;
+    }
+    double F2u, F1d;
+    two_stream(w0, dtau, B1, B2, F1u, F2d, F2u, F1d);
+    if (act) {
+      if (DIR == kAbsorb || !top) Fu[(int64_t)(i + 1) * nl + j] = F2u;
+      Fd[(int64_t)i * nl + j] = F1d;
+      if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = dtau;
+    }
+    const double y = wave_sum4(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
+    if (lane < 4) red[((int64_t)wv * ns + k) * 4 + (lane & 1) * 2 + ((lane >> 1) & 1)] = y;
+    if (DIR == kEmit) { carry = F2u; Bc = B2; } else { carry = F1d; Bc = B1; }
+  }
+  __syncthreads();
+  const int nw = kBlock / 64;
+  for (int idx = tid; idx < ns * 4; idx += kBlock) {
+    double s = red[idx];
+    for (int w = 1; w < nw; ++w) s += red[(int64_t)w * ns * 4 + idx];
+    part[(int64_t)idx * gridDim.x + blockIdx.x] = s;
   }
 }
 
@@ -205,6 +310,32 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, int dir) {
     u.steps[k] = sp;
   }
   const int nS = u.n_species;
+  if (u.fast) {
+    for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+      const int i = step_layer(dir, k, nL);
+      FastStep f;
+      f.layer = i;
+      f.top = (dir == kEmit && i == nL - 1) ? 1 : 0;
+      f.T1 = T[i];
+      f.T2 = f.top ? T[i] : T[i + 1];
+      const double p2 = f.top ? u.p_top2 : u.p[i + 1];
+      f.dm = (u.p[i] - p2) / u.g;
+      for (int s = 0; s < kMaxFastS; ++s) {
+        f.wlo[s] = f.whi[s] = f.mmr[s] = 0.0;
+        f.off[s] = 0;
+      }
+      for (int s = 0; s < nS; ++s) {
+        const TermP t = make_term(u.spec[s], u.pmeta[(int64_t)s * nL + i], u.tnodes, u.tperm,
+                                  u.mmr[(int64_t)s * nL + i], T[i], 1);
+        f.off[s] = t.row[0] - u.spec[s].tab;
+        f.wlo[s] = t.w[0];
+        f.whi[s] = t.w[1];
+        f.mmr[s] = t.mmr;
+      }
+      u.fsteps[k] = f;
+    }
+    return;
+  }
   for (int idx = threadIdx.x; idx < ns * nS; idx += blockDim.x) {
     const int k = idx / nS, s = idx % nS;
     const int i = step_layer(dir, k, nL);
@@ -370,24 +501,39 @@ static void launch_sweep_t(const SweepArgs& a, int nblocks, hipStream_t st) {
 }
 
 template <int DIR>
-static void launch_sweep_dir(const SweepArgs& a, int nblocks, bool fast, hipStream_t st) {
-  if (!fast) return launch_sweep_t<DIR, 1, false>(a, nblocks, st);
-  switch (a.n_species) {
-    case 1: return launch_sweep_t<DIR, 1, true>(a, nblocks, st);
-    case 2: return launch_sweep_t<DIR, 2, true>(a, nblocks, st);
-    case 3: return launch_sweep_t<DIR, 3, true>(a, nblocks, st);
-    case 4: return launch_sweep_t<DIR, 4, true>(a, nblocks, st);
-    case 5: return launch_sweep_t<DIR, 5, true>(a, nblocks, st);
-    case 6: return launch_sweep_t<DIR, 6, true>(a, nblocks, st);
-    case 7: return launch_sweep_t<DIR, 7, true>(a, nblocks, st);
-    case 8: return launch_sweep_t<DIR, 8, true>(a, nblocks, st);
-    default: return launch_sweep_t<DIR, 1, false>(a, nblocks, st);
-  }
+static void launch_sweep_dir(const SweepArgs& a, int nblocks, bool, hipStream_t st) {
+  launch_sweep_t<DIR, 1, false>(a, nblocks, st);
 }
 
 void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st) {
   if (dir == kEmit) launch_sweep_dir<kEmit>(a, nblocks, fast, st);
   else launch_sweep_dir<kAbsorb>(a, nblocks, fast, st);
+}
+
+template <int DIR, int S>
+static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
+  const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double);
+  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S>), dim3(nblocks), dim3(kBlock), shm, st, a,
+                     a.steps, a.F_up, a.F_down, a.part, a.dtaus);
+}
+
+template <int DIR>
+static void launch_fast_dir(int S, const FastArgs& a, int nblocks, hipStream_t st) {
+  switch (S) {
+    case 1: return launch_fast_t<DIR, 1>(a, nblocks, st);
+    case 2: return launch_fast_t<DIR, 2>(a, nblocks, st);
+    case 3: return launch_fast_t<DIR, 3>(a, nblocks, st);
+    case 4: return launch_fast_t<DIR, 4>(a, nblocks, st);
+    case 5: return launch_fast_t<DIR, 5>(a, nblocks, st);
+    case 6: return launch_fast_t<DIR, 6>(a, nblocks, st);
+    case 7: return launch_fast_t<DIR, 7>(a, nblocks, st);
+    default: return launch_fast_t<DIR, 8>(a, nblocks, st);
+  }
+}
+
+void launch_sweep_fast(int dir, int S, const FastArgs& a, int nblocks, hipStream_t st) {
+  if (dir == kEmit) launch_fast_dir<kEmit>(S, a, nblocks, st);
+  else launch_fast_dir<kAbsorb>(S, a, nblocks, st);
 }
 
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,

@@ -112,6 +112,7 @@ struct frei_ctx {
   // sweep scratch
   StepP* d_steps = nullptr;
   TermP* d_terms = nullptr;
+  FastStep* d_fsteps = nullptr;
   double *d_part = nullptr, *d_Fb = nullptr, *d_Fb_all = nullptr;
   // T-P loop state
   int* d_conv = nullptr;
@@ -124,6 +125,9 @@ struct frei_ctx {
   // comm
   void* comm = nullptr;
   int nranks = 1, rank = 0;
+  frei_allgather_fn host_ag = nullptr;  // host all-gather callback (alternative to RCCL)
+  void* host_ag_user = nullptr;
+  double* h_ag = nullptr;               // pinned [nranks + 1][n_steps * 4]
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -191,6 +195,7 @@ int build_meta(frei_ctx* c) {
       c->tperm.push_back(perm[k]);
     }
     if (m.one_T) fast = 0;
+    if (S > kMaxFastS) fast = 0;
     c->smeta[s] = m;
     // sorted pressure nodes + bracket of every layer pressure
     std::vector<int32_t> pp(q.n_p);
@@ -261,6 +266,7 @@ SetupArgs setup_args(frei_ctx* c) {
   u.mmr = c->d_mmr;
   u.steps = c->d_steps;
   u.terms = c->d_terms;
+  u.fsteps = c->d_fsteps;
   return u;
 }
 
@@ -314,13 +320,43 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     if (!e0 || !e1) return fail("hipEventCreate failed");
     HIP_TRY(hipEventRecord(e0, c->stream));
   }
-  launch_sweep(o.dir, a, c->nblocks, c->fast != 0, c->stream);
+  if (c->fast) {
+    FastArgs f{};
+    f.n_lam = c->nlam;
+    f.n_steps = ns;
+    f.force = o.force;
+    f.c1 = c->d_c1;
+    f.lk = c->d_lk;
+    f.sig = c->d_sig;
+    f.wtr = c->d_wtr;
+    f.ftoa = c->d_ftoa;
+    for (int q = 0; q < kMaxFastS; ++q) f.tab[q] = q < c->S ? c->sp[q].d_tab : nullptr;
+    f.steps = c->d_fsteps;
+    f.F_up = c->d_Fu;
+    f.F_down = c->d_Fd;
+    f.dtaus = o.dtaus;
+    f.part = c->d_part;
+    f.conv = c->d_conv;
+    launch_sweep_fast(o.dir, c->S, f, c->nblocks, c->stream);
+  } else {
+    launch_sweep(o.dir, a, c->nblocks, false, c->stream);
+  }
   HIP_TRY(hipGetLastError());
   if (c->timing) HIP_TRY(hipEventRecord(e1, c->stream));
   launch_reduce(c->d_part, c->nblocks, c->d_Fb, ns * 4, c->d_conv, o.force, c->stream);
   HIP_TRY(hipGetLastError());
   const double* Fb = c->d_Fb;
-  if (c->nranks > 1) {
+  if (c->nranks > 1 && c->host_ag) {
+    const size_t n = (size_t)ns * 4;
+    HIP_TRY(hipMemcpyAsync(c->h_ag, c->d_Fb, n * sizeof(double), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->host_ag(c->h_ag, c->h_ag + n, (int64_t)n, c->host_ag_user) != 0)
+      return fail("host all-gather callback failed");
+    HIP_TRY(hipMemcpyAsync(c->d_Fb_all, c->h_ag + n, c->nranks * n * sizeof(double),
+                           hipMemcpyHostToDevice, c->stream));
+    Fb = c->d_Fb_all;
+  } else if (c->nranks > 1) {
     Rccl* r = rccl();
     if (!r || !c->comm) return fail("RCCL communicator not initialised");
     int rc = r->allGather(c->d_Fb, c->d_Fb_all, (size_t)ns * 4, kNcclFloat64, c->comm,
@@ -430,6 +466,7 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
       (rc = dalloc(&c->d_T, NL)) || (rc = dalloc(&c->d_dT, NL)) ||
       (rc = dalloc(&c->d_bol, NL * 4)) || (rc = dalloc(&c->d_mmr, NS * NL)) ||
       (rc = dalloc(&c->d_steps, ns)) || (rc = dalloc(&c->d_terms, ns * NS)) ||
+      (rc = dalloc(&c->d_fsteps, ns)) ||
       (rc = dalloc(&c->d_part, ns * 4 * (size_t)c->nblocks)) ||
       (rc = dalloc(&c->d_Fb, ns * 4)) || (rc = dalloc(&c->d_Fb_all, ns * 4)) ||
       (rc = dalloc(&c->d_conv, 1)) || (rc = dalloc(&c->d_iter, 1)) ||
@@ -464,11 +501,13 @@ int frei_ctx_destroy(frei_ctx* c) {
                   c->d_Fb, c->d_Fb_all, c->d_Tb, c->d_Ta, c->d_hist};
   for (double* p : dd)
     if (p) (void)hipFree(p);
-  void* vv[] = {c->d_smeta, c->d_pmeta, c->d_tperm, c->d_steps, c->d_terms, c->d_conv,
+  void* vv[] = {c->d_smeta, c->d_pmeta, c->d_tperm, c->d_steps, c->d_terms, c->d_fsteps,
+                c->d_conv,
                 c->d_iter, c->d_flips, c->d_prev, c->d_ndiff};
   for (void* p : vv)
     if (p) (void)hipFree(p);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
+  if (c->h_ag) (void)hipHostFree(c->h_ag);
   for (auto e : c->flag_ev)
     if (e) (void)hipEventDestroy(e);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -503,6 +542,16 @@ int frei_set_grid(frei_ctx* c, const double* c1, const double* lk, const double*
   return 0;
 }
 
+// Ascending order of the temperature nodes: tables are stored with the T axis sorted so
+// that the upper bracket row is always the next row (row_hi = row_lo + n_lam).
+static std::vector<int32_t> t_order(const double* T_nodes, int n_T) {
+  std::vector<int32_t> perm(n_T);
+  std::iota(perm.begin(), perm.end(), 0);
+  std::stable_sort(perm.begin(), perm.end(),
+                   [&](int a, int b) { return T_nodes[a] < T_nodes[b]; });
+  return perm;
+}
+
 static int set_table_common(frei_ctx* c, int s, const double* p_nodes, int n_p,
                             const double* T_nodes, int n_T) {
   if (s < 0 || s >= c->S) return fail("species index out of range");
@@ -517,7 +566,9 @@ static int set_table_common(frei_ctx* c, int s, const double* p_nodes, int n_p,
   q.n_p = n_p;
   q.n_T = n_T;
   q.p_nodes.assign(p_nodes, p_nodes + n_p);
-  q.T_nodes.assign(T_nodes, T_nodes + n_T);
+  const std::vector<int32_t> perm = t_order(T_nodes, n_T);
+  q.T_nodes.resize(n_T);
+  for (int t = 0; t < n_T; ++t) q.T_nodes[t] = T_nodes[perm[t]];  // stored ascending
   c->meta_dirty = true;
   return 0;
 }
@@ -527,8 +578,20 @@ int frei_set_table(frei_ctx* c, int s, const double* values, const double* p_nod
   if (!c || !values || !p_nodes || !T_nodes) return fail("null argument");
   TRY(set_device(c));
   TRY(set_table_common(c, s, p_nodes, n_p, T_nodes, n_T));
-  const size_t need = (size_t)n_p * n_T * (size_t)c->nlam;
-  HIP_TRY(hipMemcpy(c->sp[s].d_tab, values, need * sizeof(double), hipMemcpyHostToDevice));
+  const std::vector<int32_t> perm = t_order(T_nodes, n_T);
+  bool ident = true;
+  for (int t = 0; t < n_T; ++t) ident = ident && perm[t] == t;
+  const size_t row = (size_t)c->nlam;
+  if (ident) {
+    HIP_TRY(hipMemcpy(c->sp[s].d_tab, values, (size_t)n_p * n_T * row * sizeof(double),
+                      hipMemcpyHostToDevice));
+  } else {
+    for (int p = 0; p < n_p; ++p)
+      for (int t = 0; t < n_T; ++t)
+        HIP_TRY(hipMemcpy(c->sp[s].d_tab + ((size_t)p * n_T + t) * row,
+                          values + ((size_t)p * n_T + perm[t]) * row, row * sizeof(double),
+                          hipMemcpyHostToDevice));
+  }
   return 0;
 }
 
@@ -538,6 +601,10 @@ int frei_set_table_separable(frei_ctx* c, int s, const double* base, const doubl
   if (!c || !base || !fp || !fT || !p_nodes || !T_nodes) return fail("null argument");
   TRY(set_device(c));
   TRY(set_table_common(c, s, p_nodes, n_p, T_nodes, n_T));
+  const std::vector<int32_t> perm = t_order(T_nodes, n_T);
+  std::vector<double> fT_sorted(n_T);
+  for (int t = 0; t < n_T; ++t) fT_sorted[t] = fT[perm[t]];
+  fT = fT_sorted.data();
   double *d_base = nullptr, *d_fp = nullptr, *d_fT = nullptr;
   TRY(dalloc(&d_base, c->nlam));
   TRY(dalloc(&d_fp, n_p));
@@ -842,6 +909,24 @@ int frei_comm_init(frei_ctx* c, int nranks, int rank, const void* id128) {
   c->rank = rank;
   dfree(c->d_Fb_all);
   TRY(dalloc(&c->d_Fb_all, (size_t)nranks * (c->nL - 1) * 4));
+  return 0;
+}
+
+int frei_comm_init_host(frei_ctx* c, int nranks, int rank, frei_allgather_fn fn, void* user) {
+  if (!c || !fn) return fail("null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail("bad rank/nranks");
+  TRY(set_device(c));
+  const size_t n = (size_t)(c->nL - 1) * 4;
+  if (c->h_ag) (void)hipHostFree(c->h_ag);
+  c->h_ag = nullptr;
+  if (hipHostMalloc((void**)&c->h_ag, (nranks + 1) * n * sizeof(double)) != hipSuccess)
+    return fail("hipHostMalloc failed");
+  dfree(c->d_Fb_all);
+  TRY(dalloc(&c->d_Fb_all, (size_t)nranks * n));
+  c->host_ag = fn;
+  c->host_ag_user = user;
+  c->nranks = nranks;
+  c->rank = rank;
   return 0;
 }
 

@@ -106,10 +106,31 @@ class Engine:
         self.mmr = N.f64(np.broadcast_to(np.asarray(mmr, dtype=float),
                                          (len(self.names), self.n_layers)))
         N.check(lib.frei_set_mmr(ctx, N.dptr(self.mmr)))
+        self._ag_keep = None
         if comm is not None:
-            nranks, rank, uid = comm
-            buf = ctypes.create_string_buffer(bytes(uid), 128)
-            N.check(lib.frei_comm_init(ctx, nranks, rank, buf))
+            self._join(comm)
+
+    def _join(self, comm):
+        """comm = ("rccl", nranks, rank, unique_id_bytes) or
+        ("host", nranks, rank, allgather(send: ndarray) -> ndarray[nranks * n])."""
+        lib = N.lib()
+        kind, nranks, rank, arg = comm
+        if kind == "rccl":
+            buf = ctypes.create_string_buffer(bytes(arg), 128)
+            N.check(lib.frei_comm_init(self._ctx, nranks, rank, buf))
+        elif kind == "host":
+            def cb(send, recv, n, _user, _fn=arg, _R=nranks):
+                try:
+                    out = np.asarray(_fn(np.ctypeslib.as_array(send, (n,)).copy()),
+                                     dtype=np.float64).ravel()
+                    np.ctypeslib.as_array(recv, (_R * n,))[:] = out
+                    return 0
+                except Exception:  # surfaced as a C error, then RuntimeError
+                    return 1
+            self._ag_keep = N.ALLGATHER_FN(cb)
+            N.check(lib.frei_comm_init_host(self._ctx, nranks, rank, self._ag_keep, None))
+        else:
+            raise ValueError(f"unknown comm kind {kind!r}")
 
     # ------------------------------------------------------------------ setup
     def _set_table(self, s, tab, sl):

@@ -137,6 +137,12 @@ int frei_propagate_fluxes(int device, int64_t n, const double* c1, const double*
 int frei_comm_unique_id(void* id128);
 int frei_comm_init(frei_ctx* ctx, int nranks, int rank, const void* id128);
 
+/* Alternative exchange for testing and for hosts without RCCL peers (e.g. several ranks
+ * sharing one GPU): per sweep the n partial sums are copied to the host and
+ * fn(send[n], recv[nranks*n], n, user) must all-gather them in rank order (returns 0). */
+typedef int (*frei_allgather_fn)(const double* send, double* recv, int64_t n, void* user);
+int frei_comm_init_host(frei_ctx* ctx, int nranks, int rank, frei_allgather_fn fn, void* user);
+
 /* Timing of the sweep kernel (HIP events on the context stream around every sweep
  * launch while enabled): total milliseconds and number of timed launches. */
 int frei_timing_enable(frei_ctx* ctx, int on);

@@ -314,7 +314,7 @@ def layer_dT(Fb, T1, T2, p1, p2, g, m_bar, alpha):
 
 # ----------------------------------------------------------------- sweeps
 def _sweep(direction, tables, T, p_bar, lam_um, F_toa, g, m_bar, alpha, F_up, F_down, mmr_fn,
-           err=None):
+           err=None, bol_fn=None):
     """One emit/absorb sweep.  ``err``: optional dict {'up','down','delta'} of absolute
     error-bound rows tracked alongside the fluxes (propagate_error_bound)."""
     nL, nlam = F_up.shape
@@ -350,7 +350,10 @@ def _sweep(direction, tables, T, p_bar, lam_um, F_toa, g, m_bar, alpha, F_up, F_
         if direction == "absorb" or i < nL - 1:
             F_up[i + 1] = F2u
         F_down[i] = F1d
-        Fb = (trapz(F2u, lam_cm), trapz(F2d, lam_cm), trapz(F1u, lam_cm), trapz(F1d, lam_cm))
+        if bol_fn is None:
+            Fb = (trapz(F2u, lam_cm), trapz(F2d, lam_cm), trapz(F1u, lam_cm), trapz(F1d, lam_cm))
+        else:  # sharded runs: caller combines slice partial sums (tests/test_distributed_cpu.py)
+            Fb = bol_fn(F2u, F2d, F1u, F1d)
         dT[i] = layer_dT(Fb, T1, T2, p1, p2, g, m_bar, alpha)
     return F_up, F_down, T - dT, np.array(dtaus), dT
 
@@ -365,7 +368,7 @@ def _mmr_fn(tables, m_bar, mmr):
 
 
 def emit(tables, T, p_bar, lam_um, F_toa, g, m_bar, alpha=1, fluxes_up=None,
-         fluxes_down=None, mmr=None, err=None):
+         fluxes_down=None, mmr=None, err=None, bol_fn=None):
     """twostream.py:290-421 with n_timesteps=1 -> (F_up, F_down, T_new, dtaus, dT)."""
     T = np.asarray(T, dtype=float)
     nL, nlam = len(p_bar), len(lam_um)
@@ -376,11 +379,11 @@ def emit(tables, T, p_bar, lam_um, F_toa, g, m_bar, alpha=1, fluxes_up=None,
     else:
         F_down = fluxes_down
     return _sweep("emit", tables, T, np.asarray(p_bar), np.asarray(lam_um), F_toa, g, m_bar,
-                  alpha, F_up, F_down, _mmr_fn(tables, m_bar, mmr), err)
+                  alpha, F_up, F_down, _mmr_fn(tables, m_bar, mmr), err, bol_fn)
 
 
 def absorb(tables, T, p_bar, lam_um, F_toa, g, m_bar, alpha=1, fluxes_up=None,
-           fluxes_down=None, mmr=None, err=None):
+           fluxes_down=None, mmr=None, err=None, bol_fn=None):
     """twostream.py:424-550 with n_timesteps=1.  fluxes_up=None -> F_up[0] = pi B(T0) (Q5)."""
     T = np.asarray(T, dtype=float)
     nL, nlam = len(p_bar), len(lam_um)
@@ -395,7 +398,7 @@ def absorb(tables, T, p_bar, lam_um, F_toa, g, m_bar, alpha=1, fluxes_up=None,
     else:
         F_down = fluxes_down
     return _sweep("absorb", tables, T, np.asarray(p_bar), np.asarray(lam_um), F_toa, g, m_bar,
-                  alpha, F_up, F_down, _mmr_fn(tables, m_bar, mmr), err)
+                  alpha, F_up, F_down, _mmr_fn(tables, m_bar, mmr), err, bol_fn)
 
 
 def converged(temp_hists, dT_absorb, n_zero_crossings, convergence_dT):
@@ -410,7 +413,7 @@ def converged(temp_hists, dT_absorb, n_zero_crossings, convergence_dT):
 
 def emission_spectrum(tables, T_init, p_bar, lam_um, F_toa, g, m_bar, alpha=1,
                       n_timesteps=1, n_zero_crossings=2, convergence_dT=3.0, mmr=None,
-                      record=None, err=None):
+                      record=None, err=None, bol_fn=None):
     """core.py:233-338 -> (spectrum, final_T, temp_hist, dtaus, F_up, F_down, n_iter)."""
     nL, nlam = len(p_bar), len(lam_um)
     F_up = np.zeros((nL, nlam))
@@ -420,12 +423,12 @@ def emission_spectrum(tables, T_init, p_bar, lam_um, F_toa, g, m_bar, alpha=1,
     it = 0
     for it in range(n_timesteps):
         F_up, F_down, T, _, dTe = emit(tables, T, p_bar, lam_um, F_toa, g, m_bar, alpha,
-                                       F_up, F_down, mmr, err)
+                                       F_up, F_down, mmr, err, bol_fn)
         if record is not None:
             record.append(("emit", F_up.copy(), F_down.copy(), dTe.copy()))
         T_before = T.copy()
         F_up, F_down, T, _, dTa = absorb(tables, T, p_bar, lam_um, F_toa, g, m_bar, alpha,
-                                         F_up, F_down, mmr, err)
+                                         F_up, F_down, mmr, err, bol_fn)
         if record is not None:
             record.append(("absorb", F_up.copy(), F_down.copy(), dTa.copy()))
         hists.append(np.stack([T_before, T], axis=1))
@@ -435,7 +438,7 @@ def emission_spectrum(tables, T_init, p_bar, lam_um, F_toa, g, m_bar, alpha=1,
     th = th.T[th[0] != 0].T
     # final emit without alpha -> alpha = 1 (Q7)
     F_up, F_down, T, dtaus, _ = emit(tables, T, p_bar, lam_um, F_toa, g, m_bar, 1,
-                                     F_up, F_down, mmr, err)
+                                     F_up, F_down, mmr, err, bol_fn)
     return F_up[-1].copy(), T, th, dtaus, F_up, F_down, it + 1
 
 

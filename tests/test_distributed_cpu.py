@@ -1,0 +1,108 @@
+"""Wavelength sharding design on CPU (gloo, world_size 2): each rank sweeps its slice
+(frei_amd.engine.partition) and all-gathers per-layer partial bolometric sums built
+with the global per-point trapezoid weights (frei_amd.engine.trapz_weights); summing
+them in rank order must reproduce the unsharded reference path."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from frei_amd.engine import partition, trapz_weights
+from oracle import frei_oracle as O
+
+G_J, M_BAR = 2478.6519476149147, 4.0142926168559996e-24
+
+
+def _problem():
+    lam, _, _ = O.wavelength_grid(0.5, 10, 777)   # odd size: uneven shards
+    p = O.pressure_grid(20, -6, np.log10(200))
+    T0 = O.temperature_grid(p, 2000.0, 0.1, 0.1)
+    rng = np.random.default_rng(5)
+    Tn = np.linspace(0.7 * T0.min(), 1.3 * T0.max(), 9)
+    tabs = {n: O.Table(O.separable_table(10 ** rng.uniform(-2, 2, lam.size), (p / 1.0) ** 0.1,
+                                         (Tn / 1000) ** 0.5), p, Tn)
+            for n in ("1H2-16O", "12C-16O")}
+    return lam, p, T0, tabs
+
+
+def _slice_tabs(tabs, lo, hi):
+    return {n: O.Table(t.values[:, :, lo:hi], t.pressure, t.temperature) for n, t in tabs.items()}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lam, p, T0, tabs = _problem()
+    lo, hi = partition(lam.size, world, rank)
+    w = trapz_weights(lam * 1e-4)[lo:hi]
+
+    def bol(F2u, F2d, F1u, F1d):
+        part = torch.tensor([np.sum(w * F2u), np.sum(w * F2d), np.sum(w * F1u),
+                             np.sum(w * F1d)], dtype=torch.float64)
+        out = [torch.empty_like(part) for _ in range(world)]
+        dist.all_gather(out, part)
+        tot = out[0].clone()
+        for r in range(1, world):     # rank order: identical on every rank
+            tot += out[r]
+        return tuple(float(x) for x in tot)
+
+    sp, T, th, dtaus, fu, fd, it = O.emission_spectrum(
+        _slice_tabs(tabs, lo, hi), T0, p, lam[lo:hi], O.F_TOA(lam[lo:hi]), G_J, M_BAR, 1,
+        n_timesteps=3, bol_fn=bol)
+    q.put((rank, lo, hi, sp, T, th))
+    dist.destroy_process_group()
+
+
+def test_two_rank_lambda_sharding_matches_unsharded():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    lam, p, T0, tabs = _problem()
+    sp, T, th, *_ = O.emission_spectrum(tabs, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1,
+                                        n_timesteps=3)
+    # every rank holds bitwise-identical temperatures
+    assert np.array_equal(res[0][4], res[1][4])
+    assert np.array_equal(res[0][5], res[1][5])
+    # and they match the unsharded run (only the bolometric summation order differs)
+    assert np.max(np.abs(res[0][4] - T) / T) < 1e-12
+    spec = np.concatenate([r[3] for r in res])
+    assert res[0][2] == res[1][1] and res[1][2] == lam.size
+    assert np.max(np.abs(spec - sp) / np.abs(sp)) < 1e-10
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (500_000, 8), (7, 7), (1000, 1)])
+def test_partition_covers_grid(n, world):
+    parts = [partition(n, world, r) for r in range(world)]
+    assert parts[0][0] == 0 and parts[-1][1] == n
+    for a, b in zip(parts, parts[1:]):
+        assert a[1] == b[0]
+    sizes = [b - a for a, b in parts]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_pointwise_trapz_weights_equal_np_trapz():
+    lam = np.logspace(np.log10(0.5), np.log10(10), 1001) * 1e-4
+    f = np.random.default_rng(0).uniform(1, 2, lam.size)
+    ref = O.trapz(f, lam)
+    w = trapz_weights(lam)
+    assert abs(np.sum(w * f) - ref) / ref < 1e-14
+    # slices sum to the whole without a halo
+    parts = [np.sum(w[a:b] * f[a:b]) for a, b in (partition(lam.size, 4, r) for r in range(4))]
+    assert abs(sum(parts) - ref) / ref < 1e-14
