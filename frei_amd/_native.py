@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfrei_hip.so")
+# FREI_HIP_LIB overrides the library path (A/B builds of the same ABI, tools/ab_sweep.py)
+LIB_PATH = os.environ.get("FREI_HIP_LIB") or os.path.join(_HERE, "libfrei_hip.so")
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)

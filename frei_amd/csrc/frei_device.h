@@ -58,8 +58,8 @@ struct TermP {
 
 // Per species metadata.
 struct SpecMeta {
-  const double* tab;  // [n_p][n_T][n_lam] device
-  int64_t n_lam;
+  const double* tab;  // [n_p][n_T][n_lam] device, rows padded to n_lam (row pitch)
+  int64_t n_lam;      // row pitch in elements
   int32_t n_p, n_T;
   int32_t t_off;      // offset of this species' sorted T nodes in tnodes/tperm
   int32_t one_T;      // single unique temperature -> pressure-only interpolation
@@ -154,7 +154,9 @@ struct SetupArgs {
 
 struct FastArgs {
   int64_t n_lam;
+  int64_t pitch;           // table row pitch (elements), even
   int n_steps, force;
+  int live_only;           // skip flux stores no later sweep reads (T-P loop only)
   const double *c1, *lk, *sig, *wtr, *ftoa;
   const double* tab[kMaxFastS];
   const FastStep* steps;
@@ -168,6 +170,7 @@ struct FastArgs {
 struct SweepArgs {
   int64_t n_lam;
   int n_steps, n_species, force;
+  int live_only;
   const double *c1, *lk, *sig, *wtr, *ftoa;
   const StepP* steps;
   const TermP* terms;
@@ -204,7 +207,8 @@ void launch_propagate(int64_t n, const double* c1, const double* lk, const doubl
 void launch_kappa(int64_t n, const TermP* terms, int nS, const double* sig, double* k,
                   hipStream_t st);
 void launch_gen_table(double* tab, const double* base, const double* fp, const double* fT,
-                      int n_p, int n_T, int64_t n_lam, double lo, double hi, hipStream_t st);
+                      int n_p, int n_T, int64_t n_lam, int64_t stride, double lo, double hi,
+                      hipStream_t st);
 void launch_fill(double* x, int64_t n, double v, hipStream_t st);
 
 }  // namespace frei

@@ -24,7 +24,11 @@ namespace frei {
 // ---------------------------------------------------------------- device math
 __device__ __forceinline__ double planck(double c1, double lk, double T) {
   // twostream.py:64-67: 2hc^2/lam^5 / expm1(hc / (lam k T))
+#ifdef FREI_MEMONLY
+  return c1 * lk * T;
+#else
   return c1 / expm1(kHC / (lk * T));
+#endif
 }
 
 // twostream.py:97-177 with g_0 = 0 (call sites 389, 518), E() of :70-94.
@@ -165,8 +169,10 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     double F2u, F1d;
     two_stream(w0, dtau, B1, B2, F1u, F2d, F2u, F1d);
     if (act) {
-      if (DIR == kAbsorb || !sp.top) Fu[(int64_t)(i + 1) * nl + j] = F2u;
-      Fd[(int64_t)i * nl + j] = F1d;
+      const bool st_up = (DIR == kEmit) ? !sp.top : (!a.live_only || i == 0);
+      const bool st_dn = (DIR == kAbsorb) || !a.live_only || sp.top;
+      if (st_up) Fu[(int64_t)(i + 1) * nl + j] = F2u;
+      if (st_dn) Fd[(int64_t)i * nl + j] = F1d;
       if (a.dtaus) a.dtaus[(int64_t)(k + 1) * nl + j] = dtau;
     }
     const double y = wave_sum4(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
@@ -186,8 +192,38 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
 // Software-pipelined: the next step's 2S table rows and its stale opposite-stream flux
 // are loaded into registers while the current step computes, so HBM latency overlaps the
 // fp64 two-stream arithmetic instead of serialising with it.
+#ifndef FREI_LB_WAVES
+#define FREI_LB_WAVES 1
+#endif
+#ifndef FREI_NT
+#define FREI_NT 0
+#endif
+#ifndef FREI_SCHED_FENCE
+#define FREI_SCHED_FENCE 0
+#endif
+#ifndef FREI_PAIRLOAD
+#define FREI_PAIRLOAD 1
+#endif
+
+// Swap a double with the neighbouring lane (lane ^ 1) through DPP quad_perm [1,0,3,2]:
+// a VALU move, no LDS round trip.
+__device__ __forceinline__ double swap_pair(double x) {
+  const int2 v = __builtin_bit_cast(int2, x);
+  int2 r;
+  r.x = __builtin_amdgcn_mov_dpp(v.x, 0xB1, 0xF, 0xF, false);
+  r.y = __builtin_amdgcn_mov_dpp(v.y, 0xB1, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, r);
+}
+__device__ __forceinline__ double stream_load(const double* p) {
+#if FREI_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 template <int DIR, int S>
-__global__ __launch_bounds__(kBlock) void sweep_fast_kernel(
+__global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     FastArgs a, const FastStep* __restrict__ st, double* __restrict__ Fu,
     double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
   if (!a.force && *a.conv) return;
@@ -205,12 +241,27 @@ __global__ __launch_bounds__(kBlock) void sweep_fast_kernel(
 
   double v[2 * S];
   double stale;
+#if FREI_PAIRLOAD
+  // Lane pair (2m, 2m+1) covers wavelengths (2m, 2m+1): the even lane loads the T_lo row,
+  // the odd lane the T_hi row, 16 B each (global_load_dwordx4, 1 KiB per wave-instruction);
+  // one DPP swap later gives every lane both rows at its own wavelength.
+  const bool odd = lane & 1;
+  const int64_t jp = j0 & ~(int64_t)1;   // pair base (rows are padded: jp + 1 < row pitch)
+  const int64_t pitch = a.pitch;
+#endif
   auto prefetch = [&](int k) {
 #pragma unroll
     for (int s = 0; s < S; ++s) {
+#if FREI_PAIRLOAD
+      const double2 q = *reinterpret_cast<const double2*>(
+          a.tab[s] + st[k].off[s] + (odd ? pitch : 0) + jp);
+      v[2 * s] = q.x;
+      v[2 * s + 1] = q.y;
+#else
       const double* r = a.tab[s] + st[k].off[s] + j;
-      v[2 * s] = __builtin_nontemporal_load(r);
-      v[2 * s + 1] = __builtin_nontemporal_load(r + nl);
+      v[2 * s] = stream_load(r);
+      v[2 * s + 1] = stream_load(r + a.pitch);
+#endif
     }
     const int i = st[k].layer;
     const double* src = (DIR == kEmit) ? (st[k].top ? a.ftoa : Fd + (int64_t)(i + 1) * nl)
@@ -233,12 +284,22 @@ __global__ __launch_bounds__(kBlock) void sweep_fast_kernel(
     double tot = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const double acc = (0.0 + v[2 * s] * st[k].wlo[s]) + v[2 * s + 1] * st[k].whi[s];
+#if FREI_PAIRLOAD
+      const double recv = swap_pair(odd ? v[2 * s] : v[2 * s + 1]);
+      const double vlo = odd ? recv : v[2 * s];
+      const double vhi = odd ? v[2 * s + 1] : recv;
+#else
+      const double vlo = v[2 * s], vhi = v[2 * s + 1];
+#endif
+      const double acc = (0.0 + vlo * st[k].wlo[s]) + vhi * st[k].whi[s];
       double ops = st[k].mmr[s] * acc;
       if (S > 1) ops = isnan(ops) ? 0.0 : ops;  // xarray nansum for S > 1 (Q8)
       tot = (s == 0) ? ops : tot + ops;
     }
     const double F_st = stale;
+#if FREI_SCHED_FENCE
+    __builtin_amdgcn_sched_barrier(0);  // combine before the next loads: one register set
+#endif
     prefetch(k + 1 < ns ? k + 1 : k);  // unconditional: keeps vmcnt waits counted
     const double kap = tot + sig;
     const double dtau = dm * kap;
@@ -256,10 +317,19 @@ __global__ __launch_bounds__(kBlock) void sweep_fast_kernel(
       F1u = F_st;
     }
     double F2u, F1d;
+#ifdef FREI_MEMONLY  // diagnostic build: same memory traffic, trivial arithmetic
+    F2u = F1u * 0.5 + w0 * dtau + B2;
+    F1d = F2d * 0.5 + B1;
+#else
     two_stream(w0, dtau, B1, B2, F1u, F2d, F2u, F1d);
+#endif
     if (act) {
-      if (DIR == kAbsorb || !top) Fu[(int64_t)(i + 1) * nl + j] = F2u;
-      Fd[(int64_t)i * nl + j] = F1d;
+      // live_only: inside the T-P loop skip the dead stores (emit's interior F_down rows
+      // are rewritten by absorb before any read, absorb's F_up rows >= 2 by the next emit).
+      const bool st_up = (DIR == kEmit) ? !top : (!a.live_only || i == 0);
+      const bool st_dn = (DIR == kAbsorb) || !a.live_only || top;
+      if (st_up) Fu[(int64_t)(i + 1) * nl + j] = F2u;
+      if (st_dn) Fd[(int64_t)i * nl + j] = F1d;
       if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = dtau;
     }
     const double y = wave_sum4(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
@@ -474,7 +544,7 @@ __global__ void kappa_kernel(int64_t n, const TermP* terms, int nS, const double
 
 __global__ void gen_table_kernel(double* tab, const double* base, const double* fp,
                                  const double* fT, int n_p, int n_T, int64_t n_lam,
-                                 double lo, double hi) {
+                                 int64_t stride, double lo, double hi) {
   const int64_t total = (int64_t)n_p * n_T * n_lam;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
@@ -483,7 +553,7 @@ __global__ void gen_table_kernel(double* tab, const double* base, const double* 
     const int t = (int)(pt % n_T);
     const int p = (int)(pt / n_T);
     const double v = (fp[p] * fT[t]) * base[l];
-    tab[idx] = fmin(fmax(v, lo), hi);  // np.clip
+    tab[pt * stride + l] = fmin(fmax(v, lo), hi);  // np.clip
   }
 }
 
@@ -566,9 +636,10 @@ void launch_kappa(int64_t n, const TermP* terms, int nS, const double* sig, doub
 }
 
 void launch_gen_table(double* tab, const double* base, const double* fp, const double* fT,
-                      int n_p, int n_T, int64_t n_lam, double lo, double hi, hipStream_t st) {
+                      int n_p, int n_T, int64_t n_lam, int64_t stride, double lo, double hi,
+                      hipStream_t st) {
   hipLaunchKernelGGL(gen_table_kernel, dim3(4096), dim3(256), 0, st, tab, base, fp, fT, n_p,
-                     n_T, n_lam, lo, hi);
+                     n_T, n_lam, stride, lo, hi);
 }
 
 void launch_fill(double* x, int64_t n, double v, hipStream_t st) {

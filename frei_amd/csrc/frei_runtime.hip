@@ -75,6 +75,7 @@ constexpr int kNcclFloat64 = 8;
 struct Species {
   double* d_tab = nullptr;
   int n_p = 0, n_T = 0;
+  int64_t stride = 0;  // row pitch in elements (n_lam rounded up to 64, zero padded)
   std::vector<double> p_nodes, T_nodes;
 };
 
@@ -175,7 +176,7 @@ int build_meta(frei_ctx* c) {
     if (!q.d_tab) return fail("opacity table of species " + std::to_string(s) + " not set");
     SpecMeta m{};
     m.tab = q.d_tab;
-    m.n_lam = c->nlam;
+    m.n_lam = q.stride;
     m.n_p = q.n_p;
     m.n_T = q.n_T;
     m.t_off = (int32_t)c->tnodes.size();
@@ -291,6 +292,7 @@ struct SweepOpts {
   double* dtaus = nullptr;    // device
   double* dT_out = nullptr;   // device
   double* bol_out = nullptr;  // device
+  int live_only = 0;          // T-P loop: skip stores no later sweep reads
 };
 
 // One sweep: K1 -> reduce -> [RCCL all-gather] -> K4/K5 (+ next setup).  Asynchronous.
@@ -301,6 +303,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   a.n_steps = ns;
   a.n_species = c->S;
   a.force = o.force;
+  a.live_only = o.live_only;
   a.c1 = c->d_c1;
   a.lk = c->d_lk;
   a.sig = c->d_sig;
@@ -323,8 +326,10 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   if (c->fast) {
     FastArgs f{};
     f.n_lam = c->nlam;
+    f.pitch = c->sp[0].stride;
     f.n_steps = ns;
     f.force = o.force;
+    f.live_only = o.live_only;
     f.c1 = c->d_c1;
     f.lk = c->d_lk;
     f.sig = c->d_sig;
@@ -558,11 +563,14 @@ static int set_table_common(frei_ctx* c, int s, const double* p_nodes, int n_p,
   if (n_p < 2) return fail("a table needs at least 2 pressure nodes");
   if (n_T < 1) return fail("a table needs at least 1 temperature node");
   Species& q = c->sp[s];
-  const size_t need = (size_t)n_p * n_T * (size_t)c->nlam;
+  const int64_t stride = (c->nlam + 63) / 64 * 64;
+  const size_t need = (size_t)n_p * n_T * (size_t)stride + 64;
   if (!q.d_tab || (size_t)q.n_p * q.n_T != (size_t)n_p * n_T) {
     dfree(q.d_tab);
     TRY(dalloc(&q.d_tab, need));
   }
+  HIP_TRY(hipMemset(q.d_tab, 0, need * sizeof(double)));  // finite padding
+  q.stride = stride;
   q.n_p = n_p;
   q.n_T = n_T;
   q.p_nodes.assign(p_nodes, p_nodes + n_p);
@@ -582,13 +590,14 @@ int frei_set_table(frei_ctx* c, int s, const double* values, const double* p_nod
   bool ident = true;
   for (int t = 0; t < n_T; ++t) ident = ident && perm[t] == t;
   const size_t row = (size_t)c->nlam;
+  const size_t pitch = (size_t)c->sp[s].stride * sizeof(double);
   if (ident) {
-    HIP_TRY(hipMemcpy(c->sp[s].d_tab, values, (size_t)n_p * n_T * row * sizeof(double),
-                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy2D(c->sp[s].d_tab, pitch, values, row * sizeof(double),
+                        row * sizeof(double), (size_t)n_p * n_T, hipMemcpyHostToDevice));
   } else {
     for (int p = 0; p < n_p; ++p)
       for (int t = 0; t < n_T; ++t)
-        HIP_TRY(hipMemcpy(c->sp[s].d_tab + ((size_t)p * n_T + t) * row,
+        HIP_TRY(hipMemcpy(c->sp[s].d_tab + ((size_t)p * n_T + t) * c->sp[s].stride,
                           values + ((size_t)p * n_T + perm[t]) * row, row * sizeof(double),
                           hipMemcpyHostToDevice));
   }
@@ -612,7 +621,8 @@ int frei_set_table_separable(frei_ctx* c, int s, const double* base, const doubl
   TRY(h2d(d_base, base, c->nlam, c->stream));
   TRY(h2d(d_fp, fp, n_p, c->stream));
   TRY(h2d(d_fT, fT, n_T, c->stream));
-  launch_gen_table(c->sp[s].d_tab, d_base, d_fp, d_fT, n_p, n_T, c->nlam, lo, hi, c->stream);
+  launch_gen_table(c->sp[s].d_tab, d_base, d_fp, d_fT, n_p, n_T, c->nlam, c->sp[s].stride, lo,
+                   hi, c->stream);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));
   dfree(d_base);
@@ -720,6 +730,7 @@ static int iterate(frei_ctx* c, int n, int nzc, double thr, double alpha, bool s
     e.next_dir = kAbsorb;
     e.track = 1;
     e.alpha = alpha;
+    e.live_only = 1;
     TRY(run_sweep(c, e));
     SweepOpts a = e;
     a.dir = kAbsorb;
