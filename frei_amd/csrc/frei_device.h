@@ -137,8 +137,27 @@ __host__ __device__ inline TermP make_term(const SpecMeta& sm, const PMeta& pm,
   return t;
 }
 
+// Fast-path term (on-node pressure, >= 2 T nodes): T_lo row offset and the two weights.
+// Same arithmetic as make_term (weights (1.0 * wp) * wT), no runtime-indexed arrays.
+__host__ __device__ inline void fast_term(const SpecMeta& sm, const PMeta& pm,
+                                          const double* tnodes, double T, int64_t& off,
+                                          double& wlo, double& whi) {
+  int it, oobT;
+  double yt;
+  bracket(tnodes + sm.t_off, sm.n_T, T, it, yt, oobT);
+  off = 0;
+  wlo = whi = 0.0;
+  if (pm.oob || oobT) return;  // fill 0: zero weights on valid rows
+  const int prow = (pm.wp_lo != 0.0) ? pm.p_lo : pm.p_hi;
+  const double wp = (pm.wp_lo != 0.0) ? pm.wp_lo : pm.wp_hi;
+  off = ((int64_t)prow * sm.n_T + it) * sm.n_lam;  // T axis stored ascending
+  wlo = (1.0 * wp) * (1.0 - yt);
+  whi = (1.0 * wp) * yt;
+}
+
 struct SetupArgs {
   int n_layers, n_species, fast;
+  int n_tnodes;            // total sorted T nodes over species (tnodes length)
   double* T;               // device temperatures [n_layers]
   const double* p;         // device pressures (dyn cm^-2)
   double p_top2, g;
@@ -196,7 +215,8 @@ struct UpdateArgs {
 
 // launchers (frei_kernels.hip)
 void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st);
-void launch_sweep_fast(int dir, int S, const FastArgs& a, int nblocks, hipStream_t st);
+void launch_sweep_fast(int dir, int S, int depth, const FastArgs& a, int nblocks,
+                       hipStream_t st);
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
                    int force, hipStream_t st);
 void launch_setup(const SetupArgs& u, int dir, hipStream_t st);

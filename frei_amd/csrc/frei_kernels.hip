@@ -198,9 +198,6 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
 #ifndef FREI_NT
 #define FREI_NT 0
 #endif
-#ifndef FREI_SCHED_FENCE
-#define FREI_SCHED_FENCE 0
-#endif
 #ifndef FREI_PAIRLOAD
 #define FREI_PAIRLOAD 1
 #endif
@@ -222,10 +219,11 @@ __device__ __forceinline__ double stream_load(const double* p) {
 #endif
 }
 
-template <int DIR, int S>
+template <int DIR, int S, int PD>
 __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     FastArgs a, const FastStep* __restrict__ st, double* __restrict__ Fu,
     double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
+  static_assert(PD == 1 || PD == 2, "prefetch depth 1 or 2");
   if (!a.force && *a.conv) return;
   extern __shared__ double red[];  // [wave][step][4]
   const int tid = threadIdx.x;
@@ -238,9 +236,6 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   const double c1 = a.c1[j], lk = a.lk[j], sig = a.sig[j];
   const double wt = act ? a.wtr[j] : 0.0;
   const int ns = a.n_steps;
-
-  double v[2 * S];
-  double stale;
 #if FREI_PAIRLOAD
   // Lane pair (2m, 2m+1) covers wavelengths (2m, 2m+1): the even lane loads the T_lo row,
   // the odd lane the T_hi row, 16 B each (global_load_dwordx4, 1 KiB per wave-instruction);
@@ -249,7 +244,9 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   const int64_t jp = j0 & ~(int64_t)1;   // pair base (rows are padded: jp + 1 < row pitch)
   const int64_t pitch = a.pitch;
 #endif
-  auto prefetch = [&](int k) {
+  // Load the 2S table rows and the stale opposite-stream flux of step k into one buffer.
+  auto load = [&](int k, double (&v)[2 * S], double& stale) {
+    k = k < ns ? k : ns - 1;  // unconditional (clamped) loads keep vmcnt waits counted
 #pragma unroll
     for (int s = 0; s < S; ++s) {
 #if FREI_PAIRLOAD
@@ -268,7 +265,6 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
                                        : Fu + (int64_t)i * nl;
     stale = src[j];
   };
-  prefetch(0);
   double carry, Bc;
   if (DIR == kEmit) {
     carry = Fu[(int64_t)st[0].layer * nl + j];
@@ -277,10 +273,13 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     carry = Fd[(int64_t)(st[0].layer + 1) * nl + j];
     Bc = planck(c1, lk, st[0].T2);
   }
-  for (int k = 0; k < ns; ++k) {
-    const int i = st[k].layer;
-    const int top = st[k].top;
-    const double T1 = st[k].T1, T2 = st[k].T2, dm = st[k].dm;
+  // One step with buffer v (holding step k), which is refilled with step k + PD.
+  auto step = [&](int k, double (&v)[2 * S], double& stale) {
+    const bool valid = k < ns;       // the last pair of a PD = 2 loop may be a dummy
+    const int kk = valid ? k : ns - 1;
+    const int i = st[kk].layer;
+    const int top = st[kk].top;
+    const double T1 = st[kk].T1, T2 = st[kk].T2, dm = st[kk].dm;
     double tot = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -291,16 +290,13 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
 #else
       const double vlo = v[2 * s], vhi = v[2 * s + 1];
 #endif
-      const double acc = (0.0 + vlo * st[k].wlo[s]) + vhi * st[k].whi[s];
-      double ops = st[k].mmr[s] * acc;
+      const double acc = (0.0 + vlo * st[kk].wlo[s]) + vhi * st[kk].whi[s];
+      double ops = st[kk].mmr[s] * acc;
       if (S > 1) ops = isnan(ops) ? 0.0 : ops;  // xarray nansum for S > 1 (Q8)
       tot = (s == 0) ? ops : tot + ops;
     }
     const double F_st = stale;
-#if FREI_SCHED_FENCE
-    __builtin_amdgcn_sched_barrier(0);  // combine before the next loads: one register set
-#endif
-    prefetch(k + 1 < ns ? k + 1 : k);  // unconditional: keeps vmcnt waits counted
+    load(k + PD, v, stale);
     const double kap = tot + sig;
     const double dtau = dm * kap;
     const double w0 = sig / (sig + kap);
@@ -323,6 +319,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
 #else
     two_stream(w0, dtau, B1, B2, F1u, F2d, F2u, F1d);
 #endif
+    if (!valid) return;
     if (act) {
       // live_only: inside the T-P loop skip the dead stores (emit's interior F_down rows
       // are rewritten by absorb before any read, absorb's F_up rows >= 2 by the next emit).
@@ -335,6 +332,18 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     const double y = wave_sum4(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
     if (lane < 4) red[((int64_t)wv * ns + k) * 4 + (lane & 1) * 2 + ((lane >> 1) & 1)] = y;
     if (DIR == kEmit) { carry = F2u; Bc = B2; } else { carry = F1d; Bc = B1; }
+  };
+  double va[2 * S], sa;
+  load(0, va, sa);
+  if constexpr (PD == 1) {
+    for (int k = 0; k < ns; ++k) step(k, va, sa);
+  } else {
+    double vb[2 * S], sb;
+    load(1, vb, sb);
+    for (int k = 0; k < ns; k += 2) {   // two buffers in flight, static register names
+      step(k, va, sa);
+      step(k + 1, vb, sb);
+    }
   }
   __syncthreads();
   const int nw = kBlock / 64;
@@ -364,7 +373,8 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
 }
 
 // ---------------------------------------------------------------- setup (T -> terms)
-__device__ void setup_sweep(const SetupArgs& u, const double* T, int dir) {
+__device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P,
+                            const double* tnodes, int dir) {
   const int nL = u.n_layers;
   const int ns = nL - 1;
   for (int k = threadIdx.x; k < ns; k += blockDim.x) {
@@ -374,8 +384,8 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, int dir) {
     sp.top = (dir == kEmit && i == nL - 1) ? 1 : 0;
     sp.T1 = T[i];
     sp.T2 = sp.top ? T[i] : T[i + 1];                         // twostream.py:358-363
-    const double p2 = sp.top ? u.p_top2 : u.p[i + 1];
-    sp.dm = (u.p[i] - p2) / u.g;
+    const double p2 = sp.top ? u.p_top2 : P[i + 1];
+    sp.dm = (P[i] - p2) / u.g;
     sp.pad = 0;
     u.steps[k] = sp;
   }
@@ -383,38 +393,43 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, int dir) {
   if (u.fast) {
     for (int k = threadIdx.x; k < ns; k += blockDim.x) {
       const int i = step_layer(dir, k, nL);
-      FastStep f;
-      f.layer = i;
-      f.top = (dir == kEmit && i == nL - 1) ? 1 : 0;
-      f.T1 = T[i];
-      f.T2 = f.top ? T[i] : T[i + 1];
-      const double p2 = f.top ? u.p_top2 : u.p[i + 1];
-      f.dm = (u.p[i] - p2) / u.g;
-      for (int s = 0; s < kMaxFastS; ++s) {
-        f.wlo[s] = f.whi[s] = f.mmr[s] = 0.0;
-        f.off[s] = 0;
+      FastStep* f = u.fsteps + k;
+      const int top = (dir == kEmit && i == nL - 1) ? 1 : 0;
+      f->layer = i;
+      f->top = top;
+      f->T1 = T[i];
+      f->T2 = top ? T[i] : T[i + 1];
+      const double p2 = top ? u.p_top2 : P[i + 1];
+      f->dm = (P[i] - p2) / u.g;
+    }
+    for (int idx = threadIdx.x; idx < ns * kMaxFastS; idx += blockDim.x) {
+      const int k = idx / kMaxFastS, s = idx % kMaxFastS;
+      FastStep* f = u.fsteps + k;
+      if (s >= nS) {
+        f->off[s] = 0;
+        f->wlo[s] = f->whi[s] = f->mmr[s] = 0.0;
+        continue;
       }
-      for (int s = 0; s < nS; ++s) {
-        const TermP t = make_term(u.spec[s], u.pmeta[(int64_t)s * nL + i], u.tnodes, u.tperm,
-                                  u.mmr[(int64_t)s * nL + i], T[i], 1);
-        f.off[s] = t.row[0] - u.spec[s].tab;
-        f.wlo[s] = t.w[0];
-        f.whi[s] = t.w[1];
-        f.mmr[s] = t.mmr;
-      }
-      u.fsteps[k] = f;
+      const int i = step_layer(dir, k, nL);
+      int64_t off;
+      double wlo, whi;
+      fast_term(u.spec[s], u.pmeta[(int64_t)s * nL + i], tnodes, T[i], off, wlo, whi);
+      f->off[s] = off;
+      f->wlo[s] = wlo;
+      f->whi[s] = whi;
+      f->mmr[s] = u.mmr[(int64_t)s * nL + i];
     }
     return;
   }
   for (int idx = threadIdx.x; idx < ns * nS; idx += blockDim.x) {
     const int k = idx / nS, s = idx % nS;
     const int i = step_layer(dir, k, nL);
-    u.terms[idx] = make_term(u.spec[s], u.pmeta[(int64_t)s * nL + i], u.tnodes, u.tperm,
+    u.terms[idx] = make_term(u.spec[s], u.pmeta[(int64_t)s * nL + i], tnodes, u.tperm,
                              u.mmr[(int64_t)s * nL + i], T[i], u.fast);
   }
 }
 
-__global__ void setup_kernel(SetupArgs u, int dir) { setup_sweep(u, u.T, dir); }
+__global__ void setup_kernel(SetupArgs u, int dir) { setup_sweep(u, u.T, u.p, u.tnodes, dir); }
 
 // ---------------------------------------------------------------- K4/K5: update
 __device__ double layer_dT(const double* Fb, double T1, double T2, double p1, double p2,
@@ -450,75 +465,87 @@ __device__ double layer_dT(const double* Fb, double T1, double T2, double p1, do
   return 1 / rho0 / cp0 * div * dt;
 }
 
+// One workgroup.  Everything it re-reads (T, p, sorted T nodes) is staged in LDS first,
+// so the dT physics, the history/convergence bookkeeping and the next sweep's bracket
+// searches run without dependent global-memory round trips.
 __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
   if (!a.force && *a.conv) return;
-  extern __shared__ double shT[];  // [n_layers] new temperatures
+  extern __shared__ double sh[];
   __shared__ int all_conv;
   const int nL = a.su.n_layers;
   const int ns = nL - 1;
   const int dir = a.dir;
+  double* sT = sh;            // [nL] temperatures (old, then new)
+  double* sdT = sh + nL;      // [nL] dT
+  double* sP = sh + 2 * nL;   // [nL] pressures
+  double* sTn = sh + 3 * nL;  // [n_tnodes] sorted T nodes of every species
   if (threadIdx.x == 0) all_conv = 1;
-  for (int l = threadIdx.x; l < nL; l += blockDim.x) shT[l] = 0.0;  // dT scratch
+  for (int l = threadIdx.x; l < nL; l += blockDim.x) {
+    sT[l] = a.su.T[l];
+    sdT[l] = 0.0;
+    sP[l] = a.su.p[l];
+  }
+  for (int q = threadIdx.x; q < a.su.n_tnodes; q += blockDim.x) sTn[q] = a.su.tnodes[q];
   __syncthreads();
   for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+    const int i = step_layer(dir, k, nL);
     double Fb[4];
     for (int q = 0; q < 4; ++q) {
       double v = a.Fb[k * 4 + q];
       for (int r = 1; r < a.nranks; ++r) v += a.Fb[(int64_t)r * ns * 4 + k * 4 + q];
       Fb[q] = v;
-      if (a.bol_out) a.bol_out[(int64_t)step_layer(dir, k, nL) * 4 + q] = v;
+      if (a.bol_out) a.bol_out[(int64_t)i * 4 + q] = v;
     }
-    const int i = step_layer(dir, k, nL);
     const bool top = (dir == kEmit && i == nL - 1);
-    const double T1 = a.su.T[i];
-    const double T2 = top ? T1 : a.su.T[i + 1];
-    const double p2 = top ? a.su.p_top2 : a.su.p[i + 1];
-    shT[i] = layer_dT(Fb, T1, T2, a.su.p[i], p2, a.su.g, a.m_bar, a.alpha);
+    const double T1 = sT[i];
+    const double T2 = top ? T1 : sT[i + 1];
+    const double p2 = top ? a.su.p_top2 : sP[i + 1];
+    sdT[i] = layer_dT(Fb, T1, T2, sP[i], p2, a.su.g, a.m_bar, a.alpha);
   }
   __syncthreads();
   // T <- T - dT for every layer (untouched layers have dT = 0, Q6)
   const int it = *a.iter;
   for (int l = threadIdx.x; l < nL; l += blockDim.x) {
-    const double dT = shT[l];
-    const double Told = a.su.T[l];
-    const double Tnew = Told - dT;
+    const double dT = sdT[l];
+    const double Tnew = sT[l] - dT;
     if (a.dT_out) a.dT_out[l] = dT;
     if (a.track) {
       if (dir == kEmit) {
         a.Tb[l] = Tnew;  // temperature entering the absorb sweep
       } else {
+        const double Tb = a.Tb[l];
         // absorb history column pair [T_before, T_after] (core.py:303-307)
         if (it < a.hist_cap) {
-          a.hist[((int64_t)it * 2 + 0) * nL + l] = a.Tb[l];
+          a.hist[((int64_t)it * 2 + 0) * nL + l] = Tb;
           a.hist[((int64_t)it * 2 + 1) * nL + l] = Tnew;
         }
         // incremental sign-flip count over the concatenated history (core.py:308-311)
-        double dseq[2];
-        int nd = 0;
-        if (it > 0) dseq[nd++] = a.Tb[l] - a.Ta[l];
-        dseq[nd++] = Tnew - a.Tb[l];
-        for (int q = 0; q < nd; ++q) {
-          const int sgn = (dseq[q] > 0) - (dseq[q] < 0);
-          if (a.ndiff[l] > 0 && sgn != a.prev_sign[l]) a.flips[l] += 1;
-          a.prev_sign[l] = sgn;
-          a.ndiff[l] += 1;
+        int flips = a.flips[l], prev = a.prev_sign[l], nd = a.ndiff[l];
+        const double d0 = Tb - a.Ta[l], d1 = Tnew - Tb;
+        for (int q = (it > 0 ? 0 : 1); q < 2; ++q) {
+          const double d = q == 0 ? d0 : d1;
+          const int sgn = (d > 0) - (d < 0);
+          if (nd > 0 && sgn != prev) ++flips;
+          prev = sgn;
+          ++nd;
         }
+        a.flips[l] = flips;
+        a.prev_sign[l] = prev;
+        a.ndiff[l] = nd;
         a.Ta[l] = Tnew;
-        const bool c = (a.flips[l] > a.n_zero_crossings) || (fabs(dT) < a.convergence_dT);
+        const bool c = (flips > a.n_zero_crossings) || (fabs(dT) < a.convergence_dT);
         if (!c) atomicAnd(&all_conv, 0);
       }
     }
     a.su.T[l] = Tnew;
+    sT[l] = Tnew;
   }
   __syncthreads();
   if (threadIdx.x == 0 && a.track && dir == kAbsorb) {
     *a.iter = it + 1;
     if (all_conv && a.stop_on_conv) *a.conv = 1;
   }
-  if (a.next_dir >= 0) {
-    __syncthreads();
-    setup_sweep(a.su, a.su.T, a.next_dir);
-  }
+  if (a.next_dir >= 0) setup_sweep(a.su, sT, sP, sTn, a.next_dir);
 }
 
 // ---------------------------------------------------------------- standalone kernels
@@ -580,30 +607,36 @@ void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream
   else launch_sweep_dir<kAbsorb>(a, nblocks, fast, st);
 }
 
-template <int DIR, int S>
+template <int DIR, int S, int PD>
 static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
   const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double);
-  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S>), dim3(nblocks), dim3(kBlock), shm, st, a,
+  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD>), dim3(nblocks), dim3(kBlock), shm, st, a,
                      a.steps, a.F_up, a.F_down, a.part, a.dtaus);
 }
 
-template <int DIR>
+template <int DIR, int PD>
 static void launch_fast_dir(int S, const FastArgs& a, int nblocks, hipStream_t st) {
   switch (S) {
-    case 1: return launch_fast_t<DIR, 1>(a, nblocks, st);
-    case 2: return launch_fast_t<DIR, 2>(a, nblocks, st);
-    case 3: return launch_fast_t<DIR, 3>(a, nblocks, st);
-    case 4: return launch_fast_t<DIR, 4>(a, nblocks, st);
-    case 5: return launch_fast_t<DIR, 5>(a, nblocks, st);
-    case 6: return launch_fast_t<DIR, 6>(a, nblocks, st);
-    case 7: return launch_fast_t<DIR, 7>(a, nblocks, st);
-    default: return launch_fast_t<DIR, 8>(a, nblocks, st);
+    case 1: return launch_fast_t<DIR, 1, PD>(a, nblocks, st);
+    case 2: return launch_fast_t<DIR, 2, PD>(a, nblocks, st);
+    case 3: return launch_fast_t<DIR, 3, PD>(a, nblocks, st);
+    case 4: return launch_fast_t<DIR, 4, PD>(a, nblocks, st);
+    case 5: return launch_fast_t<DIR, 5, PD>(a, nblocks, st);
+    case 6: return launch_fast_t<DIR, 6, PD>(a, nblocks, st);
+    case 7: return launch_fast_t<DIR, 7, PD>(a, nblocks, st);
+    default: return launch_fast_t<DIR, 8, PD>(a, nblocks, st);
   }
 }
 
-void launch_sweep_fast(int dir, int S, const FastArgs& a, int nblocks, hipStream_t st) {
-  if (dir == kEmit) launch_fast_dir<kEmit>(S, a, nblocks, st);
-  else launch_fast_dir<kAbsorb>(S, a, nblocks, st);
+void launch_sweep_fast(int dir, int S, int depth, const FastArgs& a, int nblocks,
+                       hipStream_t st) {
+  if (depth >= 2) {
+    if (dir == kEmit) launch_fast_dir<kEmit, 2>(S, a, nblocks, st);
+    else launch_fast_dir<kAbsorb, 2>(S, a, nblocks, st);
+  } else {
+    if (dir == kEmit) launch_fast_dir<kEmit, 1>(S, a, nblocks, st);
+    else launch_fast_dir<kAbsorb, 1>(S, a, nblocks, st);
+  }
 }
 
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
@@ -617,7 +650,7 @@ void launch_setup(const SetupArgs& u, int dir, hipStream_t st) {
 }
 
 void launch_update(const UpdateArgs& a, hipStream_t st) {
-  const size_t shm = (size_t)a.su.n_layers * sizeof(double);
+  const size_t shm = (3 * (size_t)a.su.n_layers + a.su.n_tnodes) * sizeof(double);
   hipLaunchKernelGGL(update_kernel, dim3(1), dim3(256), shm, st, a);
 }
 

@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -126,6 +127,7 @@ struct frei_ctx {
   // comm
   void* comm = nullptr;
   int nranks = 1, rank = 0;
+  int prefetch_depth = 0;               // 0 = automatic (FREI_PREFETCH_DEPTH overrides)
   frei_allgather_fn host_ag = nullptr;  // host all-gather callback (alternative to RCCL)
   void* host_ag_user = nullptr;
   double* h_ag = nullptr;               // pinned [nranks + 1][n_steps * 4]
@@ -263,6 +265,7 @@ SetupArgs setup_args(frei_ctx* c) {
   u.spec = c->d_smeta;
   u.pmeta = c->d_pmeta;
   u.tnodes = c->d_tnodes;
+  u.n_tnodes = (int)c->tnodes.size();
   u.tperm = c->d_tperm;
   u.mmr = c->d_mmr;
   u.steps = c->d_steps;
@@ -342,7 +345,11 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     f.dtaus = o.dtaus;
     f.part = c->d_part;
     f.conv = c->d_conv;
-    launch_sweep_fast(o.dir, c->S, f, c->nblocks, c->stream);
+    // Prefetch depth: below ~2 waves per SIMD (small per-GPU slices, e.g. 500k lambda over
+    // 8 GPUs) a second layer in flight hides HBM latency; at full occupancy one suffices.
+    const int depth = c->prefetch_depth > 0 ? c->prefetch_depth
+                                            : (c->nlam < 2 * 1024 * 64 ? 2 : 1);
+    launch_sweep_fast(o.dir, c->S, depth, f, c->nblocks, c->stream);
   } else {
     launch_sweep(o.dir, a, c->nblocks, false, c->stream);
   }
@@ -454,6 +461,7 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
   c->S = n_species;
   c->sp.resize(n_species);
   c->nblocks = (int)((n_lam + kBlock - 1) / kBlock);
+  if (const char* e = getenv("FREI_PREFETCH_DEPTH")) c->prefetch_depth = atoi(e);
   auto bail = [&](int rc) {
     frei_ctx_destroy(c);
     return rc;
