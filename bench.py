@@ -142,7 +142,7 @@ def main():
     ms_per_step = elapsed / a.steps * 1e3
 
     # ---- roofline of the dominant kernel (sweep), per launch, this rank's slice
-    bpu = bytes_per_update(S)
+    bpu = bytes_per_update(S, live_only=True)
     avg_sweep_s = (sweep_ms / max(n_sweeps, 1)) * 1e-3
     bytes_launch = bpu * (nL - 1) * (hi - lo)
     achieved = bytes_launch / avg_sweep_s
@@ -155,6 +155,14 @@ def main():
     t3 = time.perf_counter()
     rad_eq_wall = d.max(t3 - t2)
     n_iter = out["n_iter"]
+
+    # PMC traffic of the same workload (separate rocprofv3 --pmc passes, committed)
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", "traffic_sweep.json")
+    if os.path.exists(tpath):
+        t = json.load(open(tpath))
+        if t["workload"] == {"n_lam": n_lam // d.world, "n_layers": nL, "species": S}:
+            traffic, traffic_src = t, "profiles/traffic_sweep.json"
 
     cpu = None
     if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
@@ -187,8 +195,14 @@ def main():
             "rad_eq": {"iterations": n_iter, "max_iterations": a.rad_eq_max,
                        "wall_s": rad_eq_wall, "iters_per_s": n_iter / rad_eq_wall},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
-                         "unit": "GB/s", "frac": achieved / PEAK_HBM, "traffic": None,
-                         "kernel": "sweep_kernel", "bytes_per_update": bpu,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM,
+                         "traffic": traffic["hbm_B_per_launch"] if traffic else None,
+                         "traffic_unit": "B/launch (rocprofv3 PMC: 2*FETCH_SIZE+WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "traffic_over_algorithmic": traffic["traffic_over_algorithmic"]
+                         if traffic else None,
+                         "kernel": "sweep_fast_kernel", "bytes_per_update": bpu,
+                         "bytes_per_launch": bytes_launch,
                          "avg_launch_ms": avg_sweep_s * 1e3, "launches": n_sweeps},
             "cpu_baseline": cpu,
         }

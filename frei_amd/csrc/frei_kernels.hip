@@ -219,6 +219,42 @@ __device__ __forceinline__ double stream_load(const double* p) {
 #endif
 }
 
+// Carry-independent part of one step (everything in twostream.py:135-176 except the
+// terms that multiply the carried flux).  Split out so two layers' coefficients form one
+// straight-line block the scheduler interleaves (2x instruction-level parallelism per
+// wave, which is what a 1-wave-per-SIMD slice — 500k lambda over 8 GPUs — needs).
+struct StepCoef {
+  double psi, xi, ic, Xu, Xd;  // F2u = ic*((psi*F1u - xi*F2d) + Xu), F1d likewise with Xd
+  double dtau, Bnext;          // Bnext: Planck value the next layer reuses
+  double F_st;                 // stale opposite-stream flux
+  int layer, top;
+};
+
+__device__ __forceinline__ void coef_from(double w0, double dtau, double B1, double B2,
+                                          StepCoef& c) {
+  // twostream.py:139-176, same order as two_stream()
+  const double E = (w0 > 0.1) ? ((1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0)) : 1.0;
+  const double Emw = E - w0;
+  const double Tr = exp((-2.0 * sqrt(E * Emw)) * dtau);
+  const double r = sqrt(Emw / E);
+  const double zp = 0.5 * (1.0 + r);
+  const double zm = 0.5 * (1.0 - r);
+  const double Tr2 = Tr * Tr;
+  const double zm2 = zm * zm;
+  const double zp2 = zp * zp;
+  const double chi = zm2 * Tr2 - zp2;
+  const double xi = (zp * zm) * (1.0 - Tr2);
+  const double psi = (zm2 - zp2) * Tr;
+  const double pi_w = (kPi * (1.0 - w0)) / Emw;
+  const double q = ((B1 - B2) / dtau) / (2.0 * E);
+  c.psi = psi;
+  c.xi = xi;
+  c.ic = 1.0 / chi;
+  c.Xu = pi_w * ((B2 * (chi + xi) - psi * B1) + q * ((chi - psi) - xi));
+  c.Xd = pi_w * ((B1 * (chi + xi) - psi * B2) + q * ((xi + psi) - chi));
+  c.dtau = dtau;
+}
+
 template <int DIR, int S, int PD>
 __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     FastArgs a, const FastStep* __restrict__ st, double* __restrict__ Fu,
@@ -265,20 +301,12 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
                                        : Fu + (int64_t)i * nl;
     stale = src[j];
   };
-  double carry, Bc;
-  if (DIR == kEmit) {
-    carry = Fu[(int64_t)st[0].layer * nl + j];
-    Bc = planck(c1, lk, st[0].T1);
-  } else {
-    carry = Fd[(int64_t)(st[0].layer + 1) * nl + j];
-    Bc = planck(c1, lk, st[0].T2);
-  }
-  // One step with buffer v (holding step k), which is refilled with step k + PD.
-  auto step = [&](int k, double (&v)[2 * S], double& stale) {
-    const bool valid = k < ns;       // the last pair of a PD = 2 loop may be a dummy
-    const int kk = valid ? k : ns - 1;
-    const int i = st[kk].layer;
-    const int top = st[kk].top;
+  // Opacity and coefficients of step k from buffer v (then refilled with step k + PD).
+  // Bprev: emit -> B(T1) of this step, absorb -> B(T2) of this step (reuse, Q: B2 = next B1).
+  auto coef = [&](int k, double (&v)[2 * S], double& stale, double Bprev, StepCoef& c) {
+    const int kk = k < ns ? k : ns - 1;  // the last pair of a PD = 2 loop may be a dummy
+    c.layer = st[kk].layer;
+    c.top = st[kk].top;
     const double T1 = st[kk].T1, T2 = st[kk].T2, dm = st[kk].dm;
     double tot = 0.0;
 #pragma unroll
@@ -295,54 +323,77 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       if (S > 1) ops = isnan(ops) ? 0.0 : ops;  // xarray nansum for S > 1 (Q8)
       tot = (s == 0) ? ops : tot + ops;
     }
-    const double F_st = stale;
+    c.F_st = stale;
     load(k + PD, v, stale);
     const double kap = tot + sig;
     const double dtau = dm * kap;
     const double w0 = sig / (sig + kap);
-    double B1, B2, F1u, F2d;
+    double B1, B2;
     if (DIR == kEmit) {
-      B1 = Bc;
-      B2 = top ? Bc : planck(c1, lk, T2);
-      F1u = carry;
-      F2d = F_st;
+      B1 = Bprev;
+      B2 = c.top ? Bprev : planck(c1, lk, T2);
+      c.Bnext = B2;
     } else {
-      B2 = Bc;
+      B2 = Bprev;
       B1 = planck(c1, lk, T1);
-      F2d = carry;
-      F1u = F_st;
+      c.Bnext = B1;
     }
-    double F2u, F1d;
 #ifdef FREI_MEMONLY  // diagnostic build: same memory traffic, trivial arithmetic
-    F2u = F1u * 0.5 + w0 * dtau + B2;
-    F1d = F2d * 0.5 + B1;
+    c.psi = 0.5; c.xi = w0; c.ic = 1.0; c.Xu = B2 + dtau; c.Xd = B1; c.dtau = dtau;
 #else
-    two_stream(w0, dtau, B1, B2, F1u, F2d, F2u, F1d);
+    coef_from(w0, dtau, B1, B2, c);
 #endif
-    if (!valid) return;
+  };
+  // Carry-dependent finish of step k: fluxes, stores, bolometric partials.
+  double carry;
+  auto finish = [&](int k, const StepCoef& c) {
+    double F1u, F2d;
+    if (DIR == kEmit) { F1u = carry; F2d = c.F_st; } else { F2d = carry; F1u = c.F_st; }
+    const double F2u = c.ic * ((c.psi * F1u - c.xi * F2d) + c.Xu);
+    const double F1d = c.ic * ((c.psi * F2d - c.xi * F1u) + c.Xd);
+    if (k >= ns) return;
+    const int i = c.layer;
     if (act) {
       // live_only: inside the T-P loop skip the dead stores (emit's interior F_down rows
       // are rewritten by absorb before any read, absorb's F_up rows >= 2 by the next emit).
-      const bool st_up = (DIR == kEmit) ? !top : (!a.live_only || i == 0);
-      const bool st_dn = (DIR == kAbsorb) || !a.live_only || top;
+      const bool st_up = (DIR == kEmit) ? !c.top : (!a.live_only || i == 0);
+      const bool st_dn = (DIR == kAbsorb) || !a.live_only || c.top;
       if (st_up) Fu[(int64_t)(i + 1) * nl + j] = F2u;
       if (st_dn) Fd[(int64_t)i * nl + j] = F1d;
-      if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = dtau;
+      if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = c.dtau;
     }
     const double y = wave_sum4(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
     if (lane < 4) red[((int64_t)wv * ns + k) * 4 + (lane & 1) * 2 + ((lane >> 1) & 1)] = y;
-    if (DIR == kEmit) { carry = F2u; Bc = B2; } else { carry = F1d; Bc = B1; }
+    carry = (DIR == kEmit) ? F2u : F1d;
   };
+
+  double Bc;
+  if (DIR == kEmit) {
+    carry = Fu[(int64_t)st[0].layer * nl + j];
+    Bc = planck(c1, lk, st[0].T1);
+  } else {
+    carry = Fd[(int64_t)(st[0].layer + 1) * nl + j];
+    Bc = planck(c1, lk, st[0].T2);
+  }
   double va[2 * S], sa;
   load(0, va, sa);
   if constexpr (PD == 1) {
-    for (int k = 0; k < ns; ++k) step(k, va, sa);
+    for (int k = 0; k < ns; ++k) {
+      StepCoef ca;
+      coef(k, va, sa, Bc, ca);
+      Bc = ca.Bnext;
+      finish(k, ca);
+    }
   } else {
     double vb[2 * S], sb;
     load(1, vb, sb);
     for (int k = 0; k < ns; k += 2) {   // two buffers in flight, static register names
-      step(k, va, sa);
-      step(k + 1, vb, sb);
+      StepCoef ca, cb;
+      coef(k, va, sa, Bc, ca);          // both layers' coefficients: independent work
+      coef(k + 1, vb, sb, ca.Bnext, cb);
+      Bc = cb.Bnext;
+      finish(k, ca);                    // then the short carried recurrence
+      finish(k + 1, cb);
     }
   }
   __syncthreads();

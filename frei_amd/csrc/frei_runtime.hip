@@ -347,8 +347,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     f.conv = c->d_conv;
     // Prefetch depth: below ~2 waves per SIMD (small per-GPU slices, e.g. 500k lambda over
     // 8 GPUs) a second layer in flight hides HBM latency; at full occupancy one suffices.
-    const int depth = c->prefetch_depth > 0 ? c->prefetch_depth
-                                            : (c->nlam < 2 * 1024 * 64 ? 2 : 1);
+    const int depth = c->prefetch_depth > 0 ? c->prefetch_depth : 2;
     launch_sweep_fast(o.dir, c->S, depth, f, c->nblocks, c->stream);
   } else {
     launch_sweep(o.dir, a, c->nblocks, false, c->stream);

@@ -59,7 +59,9 @@ def c3(n_layers=60, n_lam=500_000, n_T=16, T_ref=1500.0, species=None, seed=42):
                 mmr=np.array(rows))
 
 
-def bytes_per_update(n_species, write_dtau=False):
+def bytes_per_update(n_species, write_dtau=False, live_only=False):
     """Algorithmic HBM bytes per (layer, wavelength) flux update:
-    stale opposite-stream read 8 + two flux writes 16 + two T-bracket rows per species."""
-    return 8 + 16 + 16 * n_species + (8 if write_dtau else 0)
+    stale opposite-stream read 8 + two flux writes 16 + two T-bracket rows per species.
+    Inside the T-P loop (live_only) one of the two flux rows per step is a dead store that
+    the engine skips, so 8 + 8 + 16 S."""
+    return 8 + (8 if live_only else 16) + 16 * n_species + (8 if write_dtau else 0)
