@@ -203,6 +203,7 @@ struct SweepArgs {
 struct UpdateArgs {
   SetupArgs su;
   int dir, next_dir, nranks, force, track, stop_on_conv, n_zero_crossings, hist_cap;
+  int meta_in_lds;         // per-(species, layer) metadata staged in LDS (small grids)
   double m_bar, alpha, convergence_dT;
   const double* Fb;        // [nranks][n_steps*4]
   double* dT_out;          // [n_layers] optional
@@ -215,8 +216,9 @@ struct UpdateArgs {
 
 // launchers (frei_kernels.hip)
 void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st);
-void launch_sweep_fast(int dir, int S, int depth, const FastArgs& a, int nblocks,
-                       hipStream_t st);
+void launch_sweep_fast(int dir, int S, int depth, bool nan_check, const FastArgs& a,
+                       int nblocks, hipStream_t st);
+void launch_nan_scan(const double* x, int64_t n, int* flag, hipStream_t st);
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
                    int force, hipStream_t st);
 void launch_setup(const SetupArgs& u, int dir, hipStream_t st);

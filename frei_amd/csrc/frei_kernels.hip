@@ -199,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
 #define FREI_NT 0
 #endif
 #ifndef FREI_PAIRLOAD
-#define FREI_PAIRLOAD 1
+#define FREI_PAIRLOAD 0  // paired 16 B loads: same bandwidth, +64 VALU selects/DPP per layer
 #endif
 
 // Swap a double with the neighbouring lane (lane ^ 1) through DPP quad_perm [1,0,3,2]:
@@ -255,7 +255,7 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
   c.dtau = dtau;
 }
 
-template <int DIR, int S, int PD>
+template <int DIR, int S, int PD, bool NANCHK>
 __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     FastArgs a, const FastStep* __restrict__ st, double* __restrict__ Fu,
     double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
@@ -320,7 +320,8 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
 #endif
       const double acc = (0.0 + vlo * st[kk].wlo[s]) + vhi * st[kk].whi[s];
       double ops = st[kk].mmr[s] * acc;
-      if (S > 1) ops = isnan(ops) ? 0.0 : ops;  // xarray nansum for S > 1 (Q8)
+      // xarray nansum for S > 1 (Q8); compiled out when the tables hold no NaN (scan at load)
+      if (NANCHK && S > 1) ops = isnan(ops) ? 0.0 : ops;
       tot = (s == 0) ? ops : tot + ops;
     }
     c.F_st = stale;
@@ -425,7 +426,8 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
 
 // ---------------------------------------------------------------- setup (T -> terms)
 __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P,
-                            const double* tnodes, int dir) {
+                            const double* tnodes, const SpecMeta* spec, const PMeta* pmeta,
+                            const double* mmr, int dir) {
   const int nL = u.n_layers;
   const int ns = nL - 1;
   for (int k = threadIdx.x; k < ns; k += blockDim.x) {
@@ -464,23 +466,25 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
       const int i = step_layer(dir, k, nL);
       int64_t off;
       double wlo, whi;
-      fast_term(u.spec[s], u.pmeta[(int64_t)s * nL + i], tnodes, T[i], off, wlo, whi);
+      fast_term(spec[s], pmeta[(int64_t)s * nL + i], tnodes, T[i], off, wlo, whi);
       f->off[s] = off;
       f->wlo[s] = wlo;
       f->whi[s] = whi;
-      f->mmr[s] = u.mmr[(int64_t)s * nL + i];
+      f->mmr[s] = mmr[(int64_t)s * nL + i];
     }
     return;
   }
   for (int idx = threadIdx.x; idx < ns * nS; idx += blockDim.x) {
     const int k = idx / nS, s = idx % nS;
     const int i = step_layer(dir, k, nL);
-    u.terms[idx] = make_term(u.spec[s], u.pmeta[(int64_t)s * nL + i], tnodes, u.tperm,
-                             u.mmr[(int64_t)s * nL + i], T[i], u.fast);
+    u.terms[idx] = make_term(spec[s], pmeta[(int64_t)s * nL + i], tnodes, u.tperm,
+                             mmr[(int64_t)s * nL + i], T[i], u.fast);
   }
 }
 
-__global__ void setup_kernel(SetupArgs u, int dir) { setup_sweep(u, u.T, u.p, u.tnodes, dir); }
+__global__ void setup_kernel(SetupArgs u, int dir) {
+  setup_sweep(u, u.T, u.p, u.tnodes, u.spec, u.pmeta, u.mmr, dir);
+}
 
 // ---------------------------------------------------------------- K4/K5: update
 __device__ double layer_dT(const double* Fb, double T1, double T2, double p1, double p2,
@@ -516,42 +520,83 @@ __device__ double layer_dT(const double* Fb, double T1, double T2, double p1, do
   return 1 / rho0 / cp0 * div * dt;
 }
 
-// One workgroup.  Everything it re-reads (T, p, sorted T nodes) is staged in LDS first,
-// so the dT physics, the history/convergence bookkeeping and the next sweep's bracket
-// searches run without dependent global-memory round trips.
+// One workgroup.  Phase 0 issues every global read the kernel needs at once (T, p, sorted
+// T nodes, the all-gathered partial sums, the T-P history state and — when it fits — the
+// per-(species, layer) interpolation metadata) into LDS; the dT physics, the convergence
+// bookkeeping and the next sweep's bracket searches then run from LDS.
+__host__ __device__ inline size_t update_lds_bytes(int nL, int ntn, int S, bool meta) {
+  size_t b = (size_t)(7 * nL + ntn + 4 * (nL - 1)) * sizeof(double) + 3 * (size_t)nL * sizeof(int);
+  b = (b + 15) & ~(size_t)15;
+  if (meta) b += (size_t)S * nL * (sizeof(PMeta) + sizeof(double)) + (size_t)S * sizeof(SpecMeta);
+  return b;
+}
+
 __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
   if (!a.force && *a.conv) return;
-  extern __shared__ double sh[];
+  extern __shared__ __attribute__((aligned(16))) double sh[];
   __shared__ int all_conv;
   const int nL = a.su.n_layers;
   const int ns = nL - 1;
   const int dir = a.dir;
-  double* sT = sh;            // [nL] temperatures (old, then new)
-  double* sdT = sh + nL;      // [nL] dT
-  double* sP = sh + 2 * nL;   // [nL] pressures
-  double* sTn = sh + 3 * nL;  // [n_tnodes] sorted T nodes of every species
+  const int S = a.su.n_species;
+  const int ntn = a.su.n_tnodes;
+  double* sT = sh;             // [nL] temperatures (old, then new)
+  double* sdT = sT + nL;       // [nL] dT
+  double* sP = sdT + nL;       // [nL] pressures
+  double* sTb = sP + nL;       // [nL] T entering the absorb sweep
+  double* sTa = sTb + nL;      // [nL] T after the previous absorb
+  double* sTn = sTa + nL;      // [ntn] sorted T nodes of every species
+  double* sFb = sTn + ntn;     // [ns * 4] rank-summed bolometric partials
+  int* sFl = reinterpret_cast<int*>(sFb + ns * 4);  // flips, prev sign, n diffs
+  int* sPv = sFl + nL;
+  int* sNd = sPv + nL;
+  const bool meta = a.meta_in_lds;
+  char* mb = reinterpret_cast<char*>(sh) + (((reinterpret_cast<char*>(sNd + nL) -
+                                              reinterpret_cast<char*>(sh)) + 15) & ~15);
+  PMeta* sPm = reinterpret_cast<PMeta*>(mb);
+  double* sMm = reinterpret_cast<double*>(sPm + (meta ? S * nL : 0));
+  SpecMeta* sSp = reinterpret_cast<SpecMeta*>(sMm + (meta ? S * nL : 0));
   if (threadIdx.x == 0) all_conv = 1;
   for (int l = threadIdx.x; l < nL; l += blockDim.x) {
     sT[l] = a.su.T[l];
     sdT[l] = 0.0;
     sP[l] = a.su.p[l];
+    if (a.track) {
+      sTb[l] = a.Tb[l];
+      sTa[l] = a.Ta[l];
+      sFl[l] = a.flips[l];
+      sPv[l] = a.prev_sign[l];
+      sNd[l] = a.ndiff[l];
+    }
   }
-  for (int q = threadIdx.x; q < a.su.n_tnodes; q += blockDim.x) sTn[q] = a.su.tnodes[q];
+  for (int q = threadIdx.x; q < ntn; q += blockDim.x) sTn[q] = a.su.tnodes[q];
+  for (int q = threadIdx.x; q < ns * 4; q += blockDim.x) {
+    double v = a.Fb[q];
+    for (int r = 1; r < a.nranks; ++r) v += a.Fb[(int64_t)r * ns * 4 + q];  // rank order
+    sFb[q] = v;
+  }
+  if (meta) {
+    for (int q = threadIdx.x; q < S * nL; q += blockDim.x) {
+      sPm[q] = a.su.pmeta[q];
+      sMm[q] = a.su.mmr[q];
+    }
+    for (int q = threadIdx.x; q < S; q += blockDim.x) sSp[q] = a.su.spec[q];
+  }
   __syncthreads();
   for (int k = threadIdx.x; k < ns; k += blockDim.x) {
     const int i = step_layer(dir, k, nL);
-    double Fb[4];
-    for (int q = 0; q < 4; ++q) {
-      double v = a.Fb[k * 4 + q];
-      for (int r = 1; r < a.nranks; ++r) v += a.Fb[(int64_t)r * ns * 4 + k * 4 + q];
-      Fb[q] = v;
-      if (a.bol_out) a.bol_out[(int64_t)i * 4 + q] = v;
-    }
+    const double* Fb = sFb + k * 4;
+    if (a.bol_out)
+      for (int q = 0; q < 4; ++q) a.bol_out[(int64_t)i * 4 + q] = Fb[q];
     const bool top = (dir == kEmit && i == nL - 1);
     const double T1 = sT[i];
     const double T2 = top ? T1 : sT[i + 1];
     const double p2 = top ? a.su.p_top2 : sP[i + 1];
+#ifdef FREI_UPD_NODT  // diagnostic ablation build
+    sdT[i] = 1e-3 * (Fb[0] - Fb[1]) + T2 * 1e-9 + p2 * 1e-20;
+#else
     sdT[i] = layer_dT(Fb, T1, T2, sP[i], p2, a.su.g, a.m_bar, a.alpha);
+#endif
   }
   __syncthreads();
   // T <- T - dT for every layer (untouched layers have dT = 0, Q6)
@@ -564,15 +609,15 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
       if (dir == kEmit) {
         a.Tb[l] = Tnew;  // temperature entering the absorb sweep
       } else {
-        const double Tb = a.Tb[l];
+        const double Tb = sTb[l];
         // absorb history column pair [T_before, T_after] (core.py:303-307)
         if (it < a.hist_cap) {
           a.hist[((int64_t)it * 2 + 0) * nL + l] = Tb;
           a.hist[((int64_t)it * 2 + 1) * nL + l] = Tnew;
         }
         // incremental sign-flip count over the concatenated history (core.py:308-311)
-        int flips = a.flips[l], prev = a.prev_sign[l], nd = a.ndiff[l];
-        const double d0 = Tb - a.Ta[l], d1 = Tnew - Tb;
+        int flips = sFl[l], prev = sPv[l], nd = sNd[l];
+        const double d0 = Tb - sTa[l], d1 = Tnew - Tb;
         for (int q = (it > 0 ? 0 : 1); q < 2; ++q) {
           const double d = q == 0 ? d0 : d1;
           const int sgn = (d > 0) - (d < 0);
@@ -596,7 +641,11 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
     *a.iter = it + 1;
     if (all_conv && a.stop_on_conv) *a.conv = 1;
   }
-  if (a.next_dir >= 0) setup_sweep(a.su, sT, sP, sTn, a.next_dir);
+#ifndef FREI_UPD_NOSETUP  // diagnostic ablation build
+  if (a.next_dir >= 0)
+    setup_sweep(a.su, sT, sP, sTn, meta ? sSp : a.su.spec, meta ? sPm : a.su.pmeta,
+                meta ? sMm : a.su.mmr, a.next_dir);
+#endif
 }
 
 // ---------------------------------------------------------------- standalone kernels
@@ -658,36 +707,54 @@ void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream
   else launch_sweep_dir<kAbsorb>(a, nblocks, fast, st);
 }
 
-template <int DIR, int S, int PD>
+template <int DIR, int S, int PD, bool NC>
 static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
   const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double);
-  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD>), dim3(nblocks), dim3(kBlock), shm, st, a,
-                     a.steps, a.F_up, a.F_down, a.part, a.dtaus);
+  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC>), dim3(nblocks), dim3(kBlock), shm, st,
+                     a, a.steps, a.F_up, a.F_down, a.part, a.dtaus);
 }
 
-template <int DIR, int PD>
+template <int DIR, int PD, bool NC>
 static void launch_fast_dir(int S, const FastArgs& a, int nblocks, hipStream_t st) {
   switch (S) {
-    case 1: return launch_fast_t<DIR, 1, PD>(a, nblocks, st);
-    case 2: return launch_fast_t<DIR, 2, PD>(a, nblocks, st);
-    case 3: return launch_fast_t<DIR, 3, PD>(a, nblocks, st);
-    case 4: return launch_fast_t<DIR, 4, PD>(a, nblocks, st);
-    case 5: return launch_fast_t<DIR, 5, PD>(a, nblocks, st);
-    case 6: return launch_fast_t<DIR, 6, PD>(a, nblocks, st);
-    case 7: return launch_fast_t<DIR, 7, PD>(a, nblocks, st);
-    default: return launch_fast_t<DIR, 8, PD>(a, nblocks, st);
+    case 1: return launch_fast_t<DIR, 1, PD, NC>(a, nblocks, st);
+    case 2: return launch_fast_t<DIR, 2, PD, NC>(a, nblocks, st);
+    case 3: return launch_fast_t<DIR, 3, PD, NC>(a, nblocks, st);
+    case 4: return launch_fast_t<DIR, 4, PD, NC>(a, nblocks, st);
+    case 5: return launch_fast_t<DIR, 5, PD, NC>(a, nblocks, st);
+    case 6: return launch_fast_t<DIR, 6, PD, NC>(a, nblocks, st);
+    case 7: return launch_fast_t<DIR, 7, PD, NC>(a, nblocks, st);
+    default: return launch_fast_t<DIR, 8, PD, NC>(a, nblocks, st);
   }
 }
 
-void launch_sweep_fast(int dir, int S, int depth, const FastArgs& a, int nblocks,
-                       hipStream_t st) {
+template <int PD, bool NC>
+static void launch_fast_pd(int dir, int S, const FastArgs& a, int nblocks, hipStream_t st) {
+  if (dir == kEmit) launch_fast_dir<kEmit, PD, NC>(S, a, nblocks, st);
+  else launch_fast_dir<kAbsorb, PD, NC>(S, a, nblocks, st);
+}
+
+void launch_sweep_fast(int dir, int S, int depth, bool nan_check, const FastArgs& a,
+                       int nblocks, hipStream_t st) {
   if (depth >= 2) {
-    if (dir == kEmit) launch_fast_dir<kEmit, 2>(S, a, nblocks, st);
-    else launch_fast_dir<kAbsorb, 2>(S, a, nblocks, st);
+    if (nan_check) launch_fast_pd<2, true>(dir, S, a, nblocks, st);
+    else launch_fast_pd<2, false>(dir, S, a, nblocks, st);
   } else {
-    if (dir == kEmit) launch_fast_dir<kEmit, 1>(S, a, nblocks, st);
-    else launch_fast_dir<kAbsorb, 1>(S, a, nblocks, st);
+    if (nan_check) launch_fast_pd<1, true>(dir, S, a, nblocks, st);
+    else launch_fast_pd<1, false>(dir, S, a, nblocks, st);
   }
+}
+
+__global__ void nan_scan_kernel(const double* __restrict__ x, int64_t n, int* flag) {
+  int found = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    found |= isnan(x[i]) ? 1 : 0;
+  if (__any(found) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+void launch_nan_scan(const double* x, int64_t n, int* flag, hipStream_t st) {
+  hipLaunchKernelGGL(nan_scan_kernel, dim3(2048), dim3(256), 0, st, x, n, flag);
 }
 
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
@@ -701,7 +768,8 @@ void launch_setup(const SetupArgs& u, int dir, hipStream_t st) {
 }
 
 void launch_update(const UpdateArgs& a, hipStream_t st) {
-  const size_t shm = (3 * (size_t)a.su.n_layers + a.su.n_tnodes) * sizeof(double);
+  const size_t shm = update_lds_bytes(a.su.n_layers, a.su.n_tnodes, a.su.n_species,
+                                      a.meta_in_lds != 0);
   hipLaunchKernelGGL(update_kernel, dim3(1), dim3(256), shm, st, a);
 }
 

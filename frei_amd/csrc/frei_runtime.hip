@@ -76,6 +76,7 @@ constexpr int kNcclFloat64 = 8;
 struct Species {
   double* d_tab = nullptr;
   int n_p = 0, n_T = 0;
+  int has_nan = 1;     // set by a device scan after upload/generation
   int64_t stride = 0;  // row pitch in elements (n_lam rounded up to 64, zero padded)
   std::vector<double> p_nodes, T_nodes;
 };
@@ -348,7 +349,9 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     // Prefetch depth: below ~2 waves per SIMD (small per-GPU slices, e.g. 500k lambda over
     // 8 GPUs) a second layer in flight hides HBM latency; at full occupancy one suffices.
     const int depth = c->prefetch_depth > 0 ? c->prefetch_depth : 2;
-    launch_sweep_fast(o.dir, c->S, depth, f, c->nblocks, c->stream);
+    bool nan_check = false;
+    for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
+    launch_sweep_fast(o.dir, c->S, depth, nan_check, f, c->nblocks, c->stream);
   } else {
     launch_sweep(o.dir, a, c->nblocks, false, c->stream);
   }
@@ -367,7 +370,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     HIP_TRY(hipMemcpyAsync(c->d_Fb_all, c->h_ag + n, c->nranks * n * sizeof(double),
                            hipMemcpyHostToDevice, c->stream));
     Fb = c->d_Fb_all;
-  } else if (c->nranks > 1) {
+  } else if (c->comm) {  // RCCL (also a forced 1-rank communicator, FREI_FORCE_RCCL=1)
     Rccl* r = rccl();
     if (!r || !c->comm) return fail("RCCL communicator not initialised");
     int rc = r->allGather(c->d_Fb, c->d_Fb_all, (size_t)ns * 4, kNcclFloat64, c->comm,
@@ -400,6 +403,10 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   u.ndiff = c->d_ndiff;
   u.iter = c->d_iter;
   u.conv = c->d_conv;
+  // metadata in LDS when the whole update stays within 64 KiB of LDS
+  u.meta_in_lds = ((size_t)c->S * c->nL * (sizeof(PMeta) + sizeof(double)) +
+                   (size_t)c->S * sizeof(SpecMeta) + (size_t)12 * c->nL * sizeof(double) +
+                   c->tnodes.size() * sizeof(double)) <= 64 * 1024;
   launch_update(u, c->stream);
   HIP_TRY(hipGetLastError());
   return 0;
@@ -588,6 +595,23 @@ static int set_table_common(frei_ctx* c, int s, const double* p_nodes, int n_p,
   return 0;
 }
 
+// Device NaN scan of species s's table: the sweep drops the per-species NaN skip of the
+// reference's nansum (Q8) when no table can produce a NaN.
+static int scan_nan(frei_ctx* c, int s) {
+  Species& q = c->sp[s];
+  int* d_flag = nullptr;
+  TRY(dalloc(&d_flag, 1));
+  HIP_TRY(hipMemsetAsync(d_flag, 0, sizeof(int), c->stream));
+  launch_nan_scan(q.d_tab, (int64_t)q.n_p * q.n_T * q.stride, d_flag, c->stream);
+  HIP_TRY(hipGetLastError());
+  int h = 1;
+  HIP_TRY(hipMemcpyAsync(&h, d_flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  dfree(d_flag);
+  q.has_nan = h;
+  return 0;
+}
+
 int frei_set_table(frei_ctx* c, int s, const double* values, const double* p_nodes, int n_p,
                    const double* T_nodes, int n_T) {
   if (!c || !values || !p_nodes || !T_nodes) return fail("null argument");
@@ -608,7 +632,7 @@ int frei_set_table(frei_ctx* c, int s, const double* values, const double* p_nod
                           values + ((size_t)p * n_T + perm[t]) * row, row * sizeof(double),
                           hipMemcpyHostToDevice));
   }
-  return 0;
+  return scan_nan(c, s);
 }
 
 int frei_set_table_separable(frei_ctx* c, int s, const double* base, const double* fp,
@@ -635,7 +659,7 @@ int frei_set_table_separable(frei_ctx* c, int s, const double* base, const doubl
   dfree(d_base);
   dfree(d_fp);
   dfree(d_fT);
-  return 0;
+  return scan_nan(c, s);
 }
 
 int frei_set_mmr(frei_ctx* c, const double* mmr) {
@@ -909,7 +933,8 @@ int frei_comm_init(frei_ctx* c, int nranks, int rank, const void* id128) {
   if (!c || !id128) return fail("null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail("bad rank/nranks");
   TRY(set_device(c));
-  if (nranks == 1) {
+  const char* force = getenv("FREI_FORCE_RCCL");
+  if (nranks == 1 && !(force && force[0] == '1')) {
     c->nranks = 1;
     c->rank = 0;
     return 0;

@@ -214,3 +214,32 @@ def test_eight_species_device_tables_match_oracle(fa):
     assert_flux_parity(up, ou, cond["up"], delta, "F_up")
     assert_flux_parity(down, od, cond["down"], delta, "F_down")
     assert row_normwise(dtaus, odt) < 1e-10
+
+
+def test_nan_in_table_is_skipped_like_xarray_sum(fa):
+    """Q8: for S > 1 the species sum skips NaN (xarray nansum); the device NaN scan must
+    switch the sweep to its NaN-checking variant."""
+    rng = np.random.default_rng(21)
+    lam, _, _ = O.wavelength_grid(0.5, 10, 640)
+    p = O.pressure_grid(16, -6, np.log10(200))
+    T0 = O.temperature_grid(p, 1800.0, 0.1, 0.1)
+    Tn = np.linspace(0.7 * T0.min(), 1.3 * T0.max(), 6)
+    names = ["1H2-16O", "12C-16O"]
+    vals = [O.separable_table(10 ** rng.uniform(-2, 1, lam.size), (p / 1.0) ** 0.1,
+                              (Tn / 1000) ** 0.5) for _ in names]
+    vals[1] = vals[1].copy()
+    vals[1][:, :, 100:140] = np.nan     # a NaN band in the second species
+    tabs_o = {n: O.Table(v, p, Tn) for n, v in zip(names, vals)}
+    tabs_f = {n: fa.OpacityTable(v, p, Tn) for n, v in zip(names, vals)}
+    k, _ = fa.kappa(tabs_f, T0[3], p[3], lam, m_bar=M_BAR)
+    ko, _ = O.kappa(tabs_o, T0[3], p[3], lam, M_BAR)
+    assert np.all(np.isfinite(k)) and rel(k, ko) < 1e-14
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), lam=lam, pressures=p, init_temperatures=T0)
+    grid.load_opacities(opacities=tabs_f)
+    spec, T, th, dtaus = grid.emission_spectrum(n_timesteps=2)
+    cond = _cond((16, lam.size))
+    osp, oT, *_ = O.emission_spectrum(tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1,
+                                      n_timesteps=2, err=cond)
+    relT = rel(T, oT)
+    assert relT < 1e-10 and np.all(np.isfinite(spec.flux))
+    assert_flux_parity(spec.flux, osp, cond["up"][-1], max(EPS, relT), "spectrum with NaN band")
