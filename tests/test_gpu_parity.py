@@ -243,3 +243,38 @@ def test_nan_in_table_is_skipped_like_xarray_sum(fa):
     relT = rel(T, oT)
     assert relT < 1e-10 and np.all(np.isfinite(spec.flux))
     assert_flux_parity(spec.flux, osp, cond["up"][-1], max(EPS, relT), "spectrum with NaN band")
+
+
+@pytest.mark.parametrize("mode", ["single_T", "offnode_p"])
+def test_generic_sweep_path_matches_oracle(fa, mode):
+    """Tables the fast kernel cannot take run the generic sweep kernel: a single-temperature
+    table (pressure-only interp1d, opacity.py:256-259) or table pressure nodes that are not
+    the grid's (full bilinear interpolation, 4 corners)."""
+    rng = np.random.default_rng(31)
+    lam, _, _ = O.wavelength_grid(0.5, 10, 900)
+    p = O.pressure_grid(18, -6, np.log10(200))
+    T0 = O.temperature_grid(p, 2000.0, 0.1, 0.1)
+    if mode == "single_T":
+        pn, Tn = p, np.array([1500.0])
+    else:
+        pn = np.logspace(np.log10(300), -7, 11)        # coarser, not on the layer grid
+        Tn = np.linspace(0.7 * T0.min(), 1.3 * T0.max(), 5)
+    names = ["1H2-16O", "12C-16O"]
+    vals = [O.separable_table(10 ** rng.uniform(-2, 1, lam.size), (pn / 1.0) ** 0.1,
+                              (Tn / 1000) ** 0.5) for _ in names]
+    tabs_o = {n: O.Table(v, pn, Tn) for n, v in zip(names, vals)}
+    tabs_f = {n: fa.OpacityTable(v, pn, Tn) for n, v in zip(names, vals)}
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), lam=lam, pressures=p, init_temperatures=T0)
+    grid.load_opacities(opacities=tabs_f)
+    spec, T, th, dtaus = grid.emission_spectrum(n_timesteps=3)
+    cond = _cond((18, lam.size))
+    osp, oT, oth, odt, ou, od, it = O.emission_spectrum(tabs_o, T0, p, lam, O.F_TOA(lam), G_J,
+                                                        M_BAR, 1, n_timesteps=3, err=cond)
+    relT = rel(T, oT)
+    assert relT < 1e-10, relT
+    delta = max(EPS, relT)
+    assert_flux_parity(spec.flux, osp, cond["up"][-1], delta, mode + " spectrum")
+    up, down = grid.engine().get_fluxes()
+    assert_flux_parity(up, ou, cond["up"], delta, mode + " F_up")
+    assert_flux_parity(down, od, cond["down"], delta, mode + " F_down")
+    assert row_normwise(dtaus, odt) < 1e-10
