@@ -46,6 +46,17 @@ struct FastStep {
   int64_t off[kMaxFastS];  // element offset of the T_lo row in species s's table
 };
 
+// Shared-bracket fast step: every species has the same pressure and temperature nodes (the
+// usual case: tables binned onto the grid), so one row offset and one weight pair serve all
+// species; 15 uniform values per step fit SGPRs and are prefetched with the table rows.
+struct FastStepS {
+  double T1, T2, dm, wlo, whi;
+  int64_t off;             // element offset of the T_lo row (same in every species table)
+  int32_t layer, top;
+  double mmr[kMaxFastS];
+};
+static_assert(sizeof(FastStepS) % sizeof(double) == 0, "FastStepS is staged as doubles");
+
 // Interpolation term of one species at one layer (opacity.py:250-263).
 struct TermP {
   const double* row[4];  // table rows (device pointers), corner order of scipy interpn
@@ -169,6 +180,8 @@ struct SetupArgs {
   StepP* steps;            // [n_layers - 1]
   TermP* terms;            // [n_layers - 1][n_species]
   FastStep* fsteps;        // [n_layers - 1] (fast path)
+  FastStepS* ssteps;       // [n_layers - 1] (fast path, shared brackets)
+  int shared;              // all species share p and T nodes
 };
 
 struct FastArgs {
@@ -179,6 +192,7 @@ struct FastArgs {
   const double *c1, *lk, *sig, *wtr, *ftoa;
   const double* tab[kMaxFastS];
   const FastStep* steps;
+  const FastStepS* ssteps;
   double* F_up;
   double* F_down;
   double* dtaus;
@@ -216,8 +230,8 @@ struct UpdateArgs {
 
 // launchers (frei_kernels.hip)
 void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st);
-void launch_sweep_fast(int dir, int S, int depth, bool nan_check, const FastArgs& a,
-                       int nblocks, hipStream_t st);
+void launch_sweep_fast(int dir, int S, int depth, bool nan_check, bool shared,
+                       const FastArgs& a, int nblocks, hipStream_t st);
 void launch_nan_scan(const double* x, int64_t n, int* flag, hipStream_t st);
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
                    int force, hipStream_t st);

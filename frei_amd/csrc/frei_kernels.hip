@@ -223,6 +223,18 @@ __device__ __forceinline__ double stream_load(const double* p) {
 // terms that multiply the carried flux).  Split out so two layers' coefficients form one
 // straight-line block the scheduler interleaves (2x instruction-level parallelism per
 // wave, which is what a 1-wave-per-SIMD slice — 500k lambda over 8 GPUs — needs).
+// Wave-uniform value read from LDS, moved to SGPRs (keeps it out of the VGPR budget).
+__device__ __forceinline__ double uni(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffLL));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int64_t uni(int64_t x) {
+  return (int64_t)__double_as_longlong(uni(__longlong_as_double((long long)x)));
+}
+
 struct StepCoef {
   double psi, xi, ic, Xu, Xd;  // F2u = ic*((psi*F1u - xi*F2d) + Xu), F1d likewise with Xd
   double dtau, Bnext;          // Bnext: Planck value the next layer reuses
@@ -255,13 +267,14 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
   c.dtau = dtau;
 }
 
-template <int DIR, int S, int PD, bool NANCHK>
+template <int DIR, int S, int PD, bool NANCHK, bool SH>
 __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
-    FastArgs a, const FastStep* __restrict__ st, double* __restrict__ Fu,
-    double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
+    FastArgs a, const FastStep* __restrict__ st, const FastStepS* __restrict__ ss,
+    double* __restrict__ Fu, double* __restrict__ Fd, double* __restrict__ part,
+    double* __restrict__ dtaus) {
   static_assert(PD == 1 || PD == 2, "prefetch depth 1 or 2");
   if (!a.force && *a.conv) return;
-  extern __shared__ double red[];  // [wave][step][4]
+  extern __shared__ double red[];  // [wave][step][4], then (shared brackets) the step table
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
@@ -272,6 +285,18 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   const double c1 = a.c1[j], lk = a.lk[j], sig = a.sig[j];
   const double wt = act ? a.wtr[j] : 0.0;
   const int ns = a.n_steps;
+  // Shared brackets: stage the whole step table (ns x 120 B) in LDS once, so every step
+  // reads its uniform parameters at LDS latency instead of scalar loads that miss the
+  // K$ and L2 of a freshly scheduled CU (the step table was written by the update kernel).
+  const FastStepS* sp = ss;
+  if constexpr (SH) {
+    double* lss = red + (int64_t)(kBlock / 64) * ns * 4;
+    const double* g = reinterpret_cast<const double*>(ss);
+    constexpr int kW = sizeof(FastStepS) / sizeof(double);
+    for (int idx = tid; idx < ns * kW; idx += kBlock) lss[idx] = g[idx];
+    __syncthreads();
+    sp = reinterpret_cast<const FastStepS*>(lss);
+  }
 #if FREI_PAIRLOAD
   // Lane pair (2m, 2m+1) covers wavelengths (2m, 2m+1): the even lane loads the T_lo row,
   // the odd lane the T_hi row, 16 B each (global_load_dwordx4, 1 KiB per wave-instruction);
@@ -280,9 +305,25 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   const int64_t jp = j0 & ~(int64_t)1;   // pair base (rows are padded: jp + 1 < row pitch)
   const int64_t pitch = a.pitch;
 #endif
-  // Load the 2S table rows and the stale opposite-stream flux of step k into one buffer.
+  // Load the 2S table rows and the stale opposite-stream flux of step k into one buffer
+  // (and, with shared brackets, the step's uniform parameters).
   auto load = [&](int k, double (&v)[2 * S], double& stale) {
     k = k < ns ? k : ns - 1;  // unconditional (clamped) loads keep vmcnt waits counted
+    if constexpr (SH) {
+      const int64_t off = uni(sp[k].off);
+      const int layer = uni(sp[k].layer);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const double* r = a.tab[s] + off + j;
+        v[2 * s] = stream_load(r);
+        v[2 * s + 1] = stream_load(r + a.pitch);
+      }
+      const double* src = (DIR == kEmit)
+                              ? (uni(sp[k].top) ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
+                              : Fu + (int64_t)layer * nl;
+      stale = src[j];
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
 #if FREI_PAIRLOAD
@@ -305,9 +346,20 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   // Bprev: emit -> B(T1) of this step, absorb -> B(T2) of this step (reuse, Q: B2 = next B1).
   auto coef = [&](int k, double (&v)[2 * S], double& stale, double Bprev, StepCoef& c) {
     const int kk = k < ns ? k : ns - 1;  // the last pair of a PD = 2 loop may be a dummy
-    c.layer = st[kk].layer;
-    c.top = st[kk].top;
-    const double T1 = st[kk].T1, T2 = st[kk].T2, dm = st[kk].dm;
+    double T1, T2, dm;
+    if constexpr (SH) {
+      c.layer = uni(sp[kk].layer);
+      c.top = uni(sp[kk].top);
+      T1 = uni(sp[kk].T1);
+      T2 = uni(sp[kk].T2);
+      dm = uni(sp[kk].dm);
+    } else {
+      c.layer = st[kk].layer;
+      c.top = st[kk].top;
+      T1 = st[kk].T1;
+      T2 = st[kk].T2;
+      dm = st[kk].dm;
+    }
     double tot = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -318,8 +370,12 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
 #else
       const double vlo = v[2 * s], vhi = v[2 * s + 1];
 #endif
-      const double acc = (0.0 + vlo * st[kk].wlo[s]) + vhi * st[kk].whi[s];
-      double ops = st[kk].mmr[s] * acc;
+      double ops;
+      if constexpr (SH) {
+        ops = uni(sp[kk].mmr[s]) * ((0.0 + vlo * uni(sp[kk].wlo)) + vhi * uni(sp[kk].whi));
+      } else {
+        ops = st[kk].mmr[s] * ((0.0 + vlo * st[kk].wlo[s]) + vhi * st[kk].whi[s]);
+      }
       // xarray nansum for S > 1 (Q8); compiled out when the tables hold no NaN (scan at load)
       if (NANCHK && S > 1) ops = isnan(ops) ? 0.0 : ops;
       tot = (s == 0) ? ops : tot + ops;
@@ -369,12 +425,16 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   };
 
   double Bc;
-  if (DIR == kEmit) {
-    carry = Fu[(int64_t)st[0].layer * nl + j];
-    Bc = planck(c1, lk, st[0].T1);
-  } else {
-    carry = Fd[(int64_t)(st[0].layer + 1) * nl + j];
-    Bc = planck(c1, lk, st[0].T2);
+  {
+    const int l0 = SH ? sp[0].layer : st[0].layer;
+    const double T10 = SH ? sp[0].T1 : st[0].T1, T20 = SH ? sp[0].T2 : st[0].T2;
+    if (DIR == kEmit) {
+      carry = Fu[(int64_t)l0 * nl + j];
+      Bc = planck(c1, lk, T10);
+    } else {
+      carry = Fd[(int64_t)(l0 + 1) * nl + j];
+      Bc = planck(c1, lk, T20);
+    }
   }
   double va[2 * S], sa;
   load(0, va, sa);
@@ -390,7 +450,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     load(1, vb, sb);
     for (int k = 0; k < ns; k += 2) {   // two buffers in flight, static register names
       StepCoef ca, cb;
-      coef(k, va, sa, Bc, ca);          // both layers' coefficients: independent work
+      coef(k, va, sa, Bc, ca);      // both layers' coefficients: independent work
       coef(k + 1, vb, sb, ca.Bnext, cb);
       Bc = cb.Bnext;
       finish(k, ca);                    // then the short carried recurrence
@@ -443,6 +503,27 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
     u.steps[k] = sp;
   }
   const int nS = u.n_species;
+  if (u.fast && u.shared) {
+    for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+      const int i = step_layer(dir, k, nL);
+      FastStepS* f = u.ssteps + k;
+      const int top = (dir == kEmit && i == nL - 1) ? 1 : 0;
+      f->layer = i;
+      f->top = top;
+      f->T1 = T[i];
+      f->T2 = top ? T[i] : T[i + 1];
+      const double p2 = top ? u.p_top2 : P[i + 1];
+      f->dm = (P[i] - p2) / u.g;
+      int64_t off;
+      double wlo, whi;
+      fast_term(spec[0], pmeta[i], tnodes, T[i], off, wlo, whi);
+      f->off = off;
+      f->wlo = wlo;
+      f->whi = whi;
+      for (int s = 0; s < kMaxFastS; ++s) f->mmr[s] = s < nS ? mmr[(int64_t)s * nL + i] : 0.0;
+    }
+    return;
+  }
   if (u.fast) {
     for (int k = threadIdx.x; k < ns; k += blockDim.x) {
       const int i = step_layer(dir, k, nL);
@@ -707,42 +788,50 @@ void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream
   else launch_sweep_dir<kAbsorb>(a, nblocks, fast, st);
 }
 
-template <int DIR, int S, int PD, bool NC>
+template <int DIR, int S, int PD, bool NC, bool SH>
 static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
-  const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double);
-  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC>), dim3(nblocks), dim3(kBlock), shm, st,
-                     a, a.steps, a.F_up, a.F_down, a.part, a.dtaus);
+  const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double) +
+                     (SH ? (size_t)a.n_steps * sizeof(FastStepS) : 0);
+  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC, SH>), dim3(nblocks), dim3(kBlock), shm,
+                     st, a, a.steps, a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
 }
 
-template <int DIR, int PD, bool NC>
+template <int DIR, int PD, bool NC, bool SH>
 static void launch_fast_dir(int S, const FastArgs& a, int nblocks, hipStream_t st) {
   switch (S) {
-    case 1: return launch_fast_t<DIR, 1, PD, NC>(a, nblocks, st);
-    case 2: return launch_fast_t<DIR, 2, PD, NC>(a, nblocks, st);
-    case 3: return launch_fast_t<DIR, 3, PD, NC>(a, nblocks, st);
-    case 4: return launch_fast_t<DIR, 4, PD, NC>(a, nblocks, st);
-    case 5: return launch_fast_t<DIR, 5, PD, NC>(a, nblocks, st);
-    case 6: return launch_fast_t<DIR, 6, PD, NC>(a, nblocks, st);
-    case 7: return launch_fast_t<DIR, 7, PD, NC>(a, nblocks, st);
-    default: return launch_fast_t<DIR, 8, PD, NC>(a, nblocks, st);
+    case 1: return launch_fast_t<DIR, 1, PD, NC, SH>(a, nblocks, st);
+    case 2: return launch_fast_t<DIR, 2, PD, NC, SH>(a, nblocks, st);
+    case 3: return launch_fast_t<DIR, 3, PD, NC, SH>(a, nblocks, st);
+    case 4: return launch_fast_t<DIR, 4, PD, NC, SH>(a, nblocks, st);
+    case 5: return launch_fast_t<DIR, 5, PD, NC, SH>(a, nblocks, st);
+    case 6: return launch_fast_t<DIR, 6, PD, NC, SH>(a, nblocks, st);
+    case 7: return launch_fast_t<DIR, 7, PD, NC, SH>(a, nblocks, st);
+    default: return launch_fast_t<DIR, 8, PD, NC, SH>(a, nblocks, st);
   }
 }
 
-template <int PD, bool NC>
+template <int PD, bool NC, bool SH>
 static void launch_fast_pd(int dir, int S, const FastArgs& a, int nblocks, hipStream_t st) {
-  if (dir == kEmit) launch_fast_dir<kEmit, PD, NC>(S, a, nblocks, st);
-  else launch_fast_dir<kAbsorb, PD, NC>(S, a, nblocks, st);
+  if (dir == kEmit) launch_fast_dir<kEmit, PD, NC, SH>(S, a, nblocks, st);
+  else launch_fast_dir<kAbsorb, PD, NC, SH>(S, a, nblocks, st);
 }
 
-void launch_sweep_fast(int dir, int S, int depth, bool nan_check, const FastArgs& a,
-                       int nblocks, hipStream_t st) {
+template <bool SH>
+static void launch_fast_sh(int dir, int S, int depth, bool nan_check, const FastArgs& a,
+                           int nblocks, hipStream_t st) {
   if (depth >= 2) {
-    if (nan_check) launch_fast_pd<2, true>(dir, S, a, nblocks, st);
-    else launch_fast_pd<2, false>(dir, S, a, nblocks, st);
+    if (nan_check) launch_fast_pd<2, true, SH>(dir, S, a, nblocks, st);
+    else launch_fast_pd<2, false, SH>(dir, S, a, nblocks, st);
   } else {
-    if (nan_check) launch_fast_pd<1, true>(dir, S, a, nblocks, st);
-    else launch_fast_pd<1, false>(dir, S, a, nblocks, st);
+    if (nan_check) launch_fast_pd<1, true, SH>(dir, S, a, nblocks, st);
+    else launch_fast_pd<1, false, SH>(dir, S, a, nblocks, st);
   }
+}
+
+void launch_sweep_fast(int dir, int S, int depth, bool nan_check, bool shared,
+                       const FastArgs& a, int nblocks, hipStream_t st) {
+  if (shared) launch_fast_sh<true>(dir, S, depth, nan_check, a, nblocks, st);
+  else launch_fast_sh<false>(dir, S, depth, nan_check, a, nblocks, st);
 }
 
 __global__ void nan_scan_kernel(const double* __restrict__ x, int64_t n, int* flag) {

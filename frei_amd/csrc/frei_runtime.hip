@@ -73,6 +73,10 @@ Rccl* rccl() {
 }
 constexpr int kNcclFloat64 = 8;
 
+#ifndef FREI_SHARED_BRACKETS
+#define FREI_SHARED_BRACKETS 1  // 0: always use per-species brackets (A/B builds)
+#endif
+
 struct Species {
   double* d_tab = nullptr;
   int n_p = 0, n_T = 0;
@@ -116,6 +120,8 @@ struct frei_ctx {
   StepP* d_steps = nullptr;
   TermP* d_terms = nullptr;
   FastStep* d_fsteps = nullptr;
+  FastStepS* d_ssteps = nullptr;
+  int shared = 0;   // fast path with one bracket for all species (identical nodes)
   double *d_part = nullptr, *d_Fb = nullptr, *d_Fb_all = nullptr;
   // T-P loop state
   int* d_conv = nullptr;
@@ -235,6 +241,14 @@ int build_meta(frei_ctx* c) {
     }
   }
   c->fast = fast;
+  // One bracket serves every species when their nodes, shapes and row pitch coincide.
+  int shared = 1;
+  for (int s = 1; s < S; ++s) {
+    const Species &q0 = c->sp[0], &q = c->sp[s];
+    shared = shared && q.n_p == q0.n_p && q.n_T == q0.n_T && q.stride == q0.stride &&
+             q.p_nodes == q0.p_nodes && q.T_nodes == q0.T_nodes;
+  }
+  c->shared = FREI_SHARED_BRACKETS ? shared : 0;
   dfree(c->d_smeta);
   dfree(c->d_pmeta);
   dfree(c->d_tnodes);
@@ -272,6 +286,8 @@ SetupArgs setup_args(frei_ctx* c) {
   u.steps = c->d_steps;
   u.terms = c->d_terms;
   u.fsteps = c->d_fsteps;
+  u.ssteps = c->d_ssteps;
+  u.shared = c->shared;
   return u;
 }
 
@@ -341,6 +357,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     f.ftoa = c->d_ftoa;
     for (int q = 0; q < kMaxFastS; ++q) f.tab[q] = q < c->S ? c->sp[q].d_tab : nullptr;
     f.steps = c->d_fsteps;
+    f.ssteps = c->d_ssteps;
     f.F_up = c->d_Fu;
     f.F_down = c->d_Fd;
     f.dtaus = o.dtaus;
@@ -351,7 +368,8 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     const int depth = c->prefetch_depth > 0 ? c->prefetch_depth : 2;
     bool nan_check = false;
     for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
-    launch_sweep_fast(o.dir, c->S, depth, nan_check, f, c->nblocks, c->stream);
+    launch_sweep_fast(o.dir, c->S, depth, nan_check, c->shared != 0, f, c->nblocks,
+                      c->stream);
   } else {
     launch_sweep(o.dir, a, c->nblocks, false, c->stream);
   }
@@ -485,7 +503,7 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
       (rc = dalloc(&c->d_T, NL)) || (rc = dalloc(&c->d_dT, NL)) ||
       (rc = dalloc(&c->d_bol, NL * 4)) || (rc = dalloc(&c->d_mmr, NS * NL)) ||
       (rc = dalloc(&c->d_steps, ns)) || (rc = dalloc(&c->d_terms, ns * NS)) ||
-      (rc = dalloc(&c->d_fsteps, ns)) ||
+      (rc = dalloc(&c->d_fsteps, ns)) || (rc = dalloc(&c->d_ssteps, ns)) ||
       (rc = dalloc(&c->d_part, ns * 4 * (size_t)c->nblocks)) ||
       (rc = dalloc(&c->d_Fb, ns * 4)) || (rc = dalloc(&c->d_Fb_all, ns * 4)) ||
       (rc = dalloc(&c->d_conv, 1)) || (rc = dalloc(&c->d_iter, 1)) ||
@@ -520,7 +538,7 @@ int frei_ctx_destroy(frei_ctx* c) {
                   c->d_Fb, c->d_Fb_all, c->d_Tb, c->d_Ta, c->d_hist};
   for (double* p : dd)
     if (p) (void)hipFree(p);
-  void* vv[] = {c->d_smeta, c->d_pmeta, c->d_tperm, c->d_steps, c->d_terms, c->d_fsteps,
+  void* vv[] = {c->d_smeta, c->d_pmeta, c->d_tperm, c->d_steps, c->d_terms, c->d_fsteps, c->d_ssteps,
                 c->d_conv,
                 c->d_iter, c->d_flips, c->d_prev, c->d_ndiff};
   for (void* p : vv)

@@ -245,25 +245,30 @@ def test_nan_in_table_is_skipped_like_xarray_sum(fa):
     assert_flux_parity(spec.flux, osp, cond["up"][-1], max(EPS, relT), "spectrum with NaN band")
 
 
-@pytest.mark.parametrize("mode", ["single_T", "offnode_p"])
+@pytest.mark.parametrize("mode", ["single_T", "offnode_p", "mixed_T"])
 def test_generic_sweep_path_matches_oracle(fa, mode):
     """Tables the fast kernel cannot take run the generic sweep kernel: a single-temperature
     table (pressure-only interp1d, opacity.py:256-259) or table pressure nodes that are not
-    the grid's (full bilinear interpolation, 4 corners)."""
+    the grid's (full bilinear interpolation, 4 corners). "mixed_T": species with different
+    temperature nodes run the fast kernel with one bracket per species (no shared bracket)."""
     rng = np.random.default_rng(31)
     lam, _, _ = O.wavelength_grid(0.5, 10, 900)
     p = O.pressure_grid(18, -6, np.log10(200))
     T0 = O.temperature_grid(p, 2000.0, 0.1, 0.1)
-    if mode == "single_T":
-        pn, Tn = p, np.array([1500.0])
-    else:
-        pn = np.logspace(np.log10(300), -7, 11)        # coarser, not on the layer grid
-        Tn = np.linspace(0.7 * T0.min(), 1.3 * T0.max(), 5)
     names = ["1H2-16O", "12C-16O"]
+    if mode == "single_T":
+        pn, Tns = p, [np.array([1500.0])] * 2
+    elif mode == "offnode_p":
+        pn = np.logspace(np.log10(300), -7, 11)        # coarser, not on the layer grid
+        Tns = [np.linspace(0.7 * T0.min(), 1.3 * T0.max(), 5)] * 2
+    else:
+        pn = p
+        Tns = [np.linspace(0.7 * T0.min(), 1.3 * T0.max(), 5),
+               np.linspace(0.6 * T0.min(), 1.4 * T0.max(), 7)]
     vals = [O.separable_table(10 ** rng.uniform(-2, 1, lam.size), (pn / 1.0) ** 0.1,
-                              (Tn / 1000) ** 0.5) for _ in names]
-    tabs_o = {n: O.Table(v, pn, Tn) for n, v in zip(names, vals)}
-    tabs_f = {n: fa.OpacityTable(v, pn, Tn) for n, v in zip(names, vals)}
+                              (Tn / 1000) ** 0.5) for Tn in Tns]
+    tabs_o = {n: O.Table(v, pn, Tn) for n, v, Tn in zip(names, vals, Tns)}
+    tabs_f = {n: fa.OpacityTable(v, pn, Tn) for n, v, Tn in zip(names, vals, Tns)}
     grid = fa.Grid(fa.Planet.from_hot_jupiter(), lam=lam, pressures=p, init_temperatures=T0)
     grid.load_opacities(opacities=tabs_f)
     spec, T, th, dtaus = grid.emission_spectrum(n_timesteps=3)
