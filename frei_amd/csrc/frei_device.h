@@ -220,6 +220,7 @@ struct UpdateArgs {
   int meta_in_lds;         // per-(species, layer) metadata staged in LDS (small grids)
   double m_bar, alpha, convergence_dT;
   const double* Fb;        // [nranks][n_steps*4]
+  const double* lnp;       // [n_layers] log(p_l / p_{l+1}) (top: emit's p_2)
   double* dT_out;          // [n_layers] optional
   double* bol_out;         // [n_layers][4] optional
   double *Tb, *Ta, *hist;
@@ -236,6 +237,7 @@ void launch_nan_scan(const double* x, int64_t n, int* flag, hipStream_t st);
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
                    int force, hipStream_t st);
 void launch_setup(const SetupArgs& u, int dir, hipStream_t st);
+void launch_log_ratio(const double* p, double p_top2, int nL, double* lnp, hipStream_t st);
 void launch_update(const UpdateArgs& a, hipStream_t st);
 void launch_propagate(int64_t n, const double* c1, const double* lk, const double* F1u,
                       const double* F2d, double T1, double T2, const double* dtau,

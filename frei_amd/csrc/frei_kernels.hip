@@ -471,17 +471,28 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
                                                      int nblocks, double* __restrict__ Fb,
                                                      const int* conv, int force) {
   if (!force && *conv) return;
-  __shared__ double sh[256];
+  __shared__ double sh[4];
   const double* p = part + (int64_t)blockIdx.x * nblocks;
   double acc = 0.0;
   for (int b = threadIdx.x; b < nblocks; b += 256) acc += p[b];
-  sh[threadIdx.x] = acc;
+  // fixed-order butterfly inside each wave, then the 4 wave sums in order: deterministic
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) Fb[blockIdx.x] = sh[0];
+  if (threadIdx.x == 0) Fb[blockIdx.x] = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+
+// ln(p_l / p_{l+1}) per layer, the top entry with emit's extrapolated p_2 (twostream.py:
+// 359, 180-187): constant over a run, so the update kernel's dT chain starts after it.
+__global__ void log_ratio_kernel(const double* __restrict__ p, double p_top2, int nL,
+                                 double* __restrict__ lnp) {
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l < nL) lnp[l] = log(p[l] / (l == nL - 1 ? p_top2 : p[l + 1]));
+}
+
+void launch_log_ratio(const double* p, double p_top2, int nL, double* lnp, hipStream_t st) {
+  hipLaunchKernelGGL(log_ratio_kernel, dim3((nL + 255) / 256), dim3(256), 0, st, p, p_top2,
+                     nL, lnp);
 }
 
 // ---------------------------------------------------------------- setup (T -> terms)
@@ -490,18 +501,6 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
                             const double* mmr, int dir) {
   const int nL = u.n_layers;
   const int ns = nL - 1;
-  for (int k = threadIdx.x; k < ns; k += blockDim.x) {
-    const int i = step_layer(dir, k, nL);
-    StepP sp;
-    sp.layer = i;
-    sp.top = (dir == kEmit && i == nL - 1) ? 1 : 0;
-    sp.T1 = T[i];
-    sp.T2 = sp.top ? T[i] : T[i + 1];                         // twostream.py:358-363
-    const double p2 = sp.top ? u.p_top2 : P[i + 1];
-    sp.dm = (P[i] - p2) / u.g;
-    sp.pad = 0;
-    u.steps[k] = sp;
-  }
   const int nS = u.n_species;
   if (u.fast && u.shared) {
     for (int k = threadIdx.x; k < ns; k += blockDim.x) {
@@ -555,6 +554,18 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
     }
     return;
   }
+  for (int k = threadIdx.x; k < ns; k += blockDim.x) {   // generic kernel's step records
+    const int i = step_layer(dir, k, nL);
+    StepP sp;
+    sp.layer = i;
+    sp.top = (dir == kEmit && i == nL - 1) ? 1 : 0;
+    sp.T1 = T[i];
+    sp.T2 = sp.top ? T[i] : T[i + 1];                         // twostream.py:358-363
+    const double p2 = sp.top ? u.p_top2 : P[i + 1];
+    sp.dm = (P[i] - p2) / u.g;
+    sp.pad = 0;
+    u.steps[k] = sp;
+  }
   for (int idx = threadIdx.x; idx < ns * nS; idx += blockDim.x) {
     const int k = idx / nS, s = idx % nS;
     const int i = step_layer(dir, k, nL);
@@ -569,10 +580,10 @@ __global__ void setup_kernel(SetupArgs u, int dir) {
 
 // ---------------------------------------------------------------- K4/K5: update
 __device__ double layer_dT(const double* Fb, double T1, double T2, double p1, double p2,
-                           double g, double m_bar, double alpha) {
-  // div_bol_net_flux (twostream.py:190-205)
+                           double lnp, double g, double m_bar, double alpha) {
+  // div_bol_net_flux (twostream.py:190-205); lnp = log(p1 / p2) (log_ratio_kernel)
   const double dF_rad = (Fb[0] - Fb[1]) - (Fb[2] - Fb[3]);
-  const double dz = (kKB * T1) / (m_bar * g) * log(p1 / p2);          // :180-187
+  const double dz = (kKB * T1) / (m_bar * g) * lnp;                   // :180-187
   const double cp = (2 + 5) / (2 * m_bar) * kKB;                      // :220-224
   const double rho = ((p1 - p2) / g) / dz;                            // :234-238
   const double dg = (T1 - T2) / dz - g / cp;                          // :241-266
@@ -595,7 +606,7 @@ __device__ double layer_dT(const double* Fb, double T1, double T2, double p1, do
   }
   // delta_temperature with the default m_bar (:208-217, Q7)
   const double m0 = kMbarDefault;
-  const double dz0 = (kKB * T1) / (m0 * g) * log(p1 / p2);
+  const double dz0 = (kKB * T1) / (m0 * g) * lnp;
   const double rho0 = ((p1 - p2) / g) / dz0;
   const double cp0 = (2 + 5) / (2 * m0) * kKB;
   return 1 / rho0 / cp0 * div * dt;
@@ -606,7 +617,7 @@ __device__ double layer_dT(const double* Fb, double T1, double T2, double p1, do
 // per-(species, layer) interpolation metadata) into LDS; the dT physics, the convergence
 // bookkeeping and the next sweep's bracket searches then run from LDS.
 __host__ __device__ inline size_t update_lds_bytes(int nL, int ntn, int S, bool meta) {
-  size_t b = (size_t)(7 * nL + ntn + 4 * (nL - 1)) * sizeof(double) + 3 * (size_t)nL * sizeof(int);
+  size_t b = (size_t)(8 * nL + ntn + 4 * (nL - 1)) * sizeof(double) + 3 * (size_t)nL * sizeof(int);
   b = (b + 15) & ~(size_t)15;
   if (meta) b += (size_t)S * nL * (sizeof(PMeta) + sizeof(double)) + (size_t)S * sizeof(SpecMeta);
   return b;
@@ -626,7 +637,8 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
   double* sP = sdT + nL;       // [nL] pressures
   double* sTb = sP + nL;       // [nL] T entering the absorb sweep
   double* sTa = sTb + nL;      // [nL] T after the previous absorb
-  double* sTn = sTa + nL;      // [ntn] sorted T nodes of every species
+  double* sLn = sTa + nL;      // [nL] log(p_l / p_{l+1}), top entry for emit
+  double* sTn = sLn + nL;      // [ntn] sorted T nodes of every species
   double* sFb = sTn + ntn;     // [ns * 4] rank-summed bolometric partials
   int* sFl = reinterpret_cast<int*>(sFb + ns * 4);  // flips, prev sign, n diffs
   int* sPv = sFl + nL;
@@ -642,6 +654,7 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
     sT[l] = a.su.T[l];
     sdT[l] = 0.0;
     sP[l] = a.su.p[l];
+    sLn[l] = a.lnp[l];
     if (a.track) {
       sTb[l] = a.Tb[l];
       sTa[l] = a.Ta[l];
@@ -676,7 +689,7 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
 #ifdef FREI_UPD_NODT  // diagnostic ablation build
     sdT[i] = 1e-3 * (Fb[0] - Fb[1]) + T2 * 1e-9 + p2 * 1e-20;
 #else
-    sdT[i] = layer_dT(Fb, T1, T2, sP[i], p2, a.su.g, a.m_bar, a.alpha);
+    sdT[i] = layer_dT(Fb, T1, T2, sP[i], p2, sLn[i], a.su.g, a.m_bar, a.alpha);
 #endif
   }
   __syncthreads();

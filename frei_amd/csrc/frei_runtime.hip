@@ -95,7 +95,7 @@ struct frei_ctx {
   int nblocks = 0;
   // grid
   double *d_c1 = nullptr, *d_lk = nullptr, *d_sig = nullptr, *d_ftoa = nullptr,
-         *d_wtr = nullptr, *d_p = nullptr;
+         *d_wtr = nullptr, *d_p = nullptr, *d_lnp = nullptr;
   std::vector<double> p;
   double p_top2 = 0, g = 0, m_bar = 0;
   bool grid_set = false;
@@ -411,6 +411,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   u.alpha = o.alpha;
   u.convergence_dT = o.convergence_dT;
   u.Fb = Fb;
+  u.lnp = c->d_lnp;
   u.dT_out = o.dT_out;
   u.bol_out = o.bol_out;
   u.Tb = c->d_Tb;
@@ -498,7 +499,7 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
   const size_t F = NL * (size_t)n_lam;
   if ((rc = dalloc(&c->d_c1, n_lam)) || (rc = dalloc(&c->d_lk, n_lam)) ||
       (rc = dalloc(&c->d_sig, n_lam)) || (rc = dalloc(&c->d_ftoa, n_lam)) ||
-      (rc = dalloc(&c->d_wtr, n_lam)) || (rc = dalloc(&c->d_p, NL)) ||
+      (rc = dalloc(&c->d_wtr, n_lam)) || (rc = dalloc(&c->d_p, NL)) || (rc = dalloc(&c->d_lnp, NL)) ||
       (rc = dalloc(&c->d_Fu, F)) || (rc = dalloc(&c->d_Fd, F)) ||
       (rc = dalloc(&c->d_T, NL)) || (rc = dalloc(&c->d_dT, NL)) ||
       (rc = dalloc(&c->d_bol, NL * 4)) || (rc = dalloc(&c->d_mmr, NS * NL)) ||
@@ -533,14 +534,13 @@ int frei_ctx_destroy(frei_ctx* c) {
     if (r && r->commDestroy) r->commDestroy(c->comm);
   }
   for (auto& s : c->sp) dfree(s.d_tab);
-  double* dd[] = {c->d_c1, c->d_lk, c->d_sig, c->d_ftoa, c->d_wtr, c->d_p, c->d_Fu, c->d_Fd,
-                  c->d_T, c->d_dT, c->d_dtaus, c->d_bol, c->d_tnodes, c->d_mmr, c->d_part,
+  double* dd[] = {c->d_c1, c->d_lk, c->d_sig, c->d_ftoa, c->d_wtr, c->d_p, c->d_lnp,
+                  c->d_Fu, c->d_Fd, c->d_T, c->d_dT, c->d_dtaus, c->d_bol, c->d_tnodes, c->d_mmr, c->d_part,
                   c->d_Fb, c->d_Fb_all, c->d_Tb, c->d_Ta, c->d_hist};
   for (double* p : dd)
     if (p) (void)hipFree(p);
-  void* vv[] = {c->d_smeta, c->d_pmeta, c->d_tperm, c->d_steps, c->d_terms, c->d_fsteps, c->d_ssteps,
-                c->d_conv,
-                c->d_iter, c->d_flips, c->d_prev, c->d_ndiff};
+  void* vv[] = {c->d_smeta, c->d_pmeta, c->d_tperm, c->d_steps, c->d_terms, c->d_fsteps,
+                c->d_ssteps, c->d_conv, c->d_iter, c->d_flips, c->d_prev, c->d_ndiff};
   for (void* p : vv)
     if (p) (void)hipFree(p);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
@@ -573,6 +573,7 @@ int frei_set_grid(frei_ctx* c, const double* c1, const double* lk, const double*
   TRY(h2d(c->d_ftoa, f_toa, n, c->stream));
   TRY(h2d(c->d_wtr, trapz_w, n, c->stream));
   TRY(h2d(c->d_p, c->p.data(), c->nL, c->stream));
+  launch_log_ratio(c->d_p, c->p_top2, c->nL, c->d_lnp, c->stream);
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->grid_set = true;
   c->meta_dirty = true;

@@ -2,17 +2,37 @@
 from the no-op launches the device-resident T-P loop issues after convergence (kernels
 that see the convergence flag return immediately; the host polls one chunk behind).
 
-    python tools/trace_summary.py run_kernel_trace.csv [bench.json]
+    python tools/trace_summary.py run_kernel_trace.csv|rocprof_dir|run_results.db [bench.json]
+
+rocprofv3 7.x writes an SQLite database by default (no --output-format csv); both are read.
 """
+import glob
+import os
+import sqlite3
 import csv
 import json
 import statistics as st
 import sys
 
 
-def main():
-    rows = list(csv.DictReader(open(sys.argv[1])))
+def load(path):
+    """Kernel dispatches as dicts with Kernel_Name / Start_Timestamp / End_Timestamp (ns)."""
+    if os.path.isdir(path):
+        cands = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True) or \
+            glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
+        path = cands[0]
+    if path.endswith(".db"):
+        con = sqlite3.connect(path)
+        rows = [dict(Kernel_Name=n, Start_Timestamp=a, End_Timestamp=b)
+                for n, a, b in con.execute("select name, start, end from kernels")]
+    else:
+        rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    return rows
+
+
+def main():
+    rows = load(sys.argv[1])
     by = {}
     for r in rows:
         by.setdefault(r["Kernel_Name"], []).append(
