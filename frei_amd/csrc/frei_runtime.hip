@@ -73,10 +73,6 @@ Rccl* rccl() {
 }
 constexpr int kNcclFloat64 = 8;
 
-#ifndef FREI_SHARED_BRACKETS
-#define FREI_SHARED_BRACKETS 1  // 0: always use per-species brackets (A/B builds)
-#endif
-
 struct Species {
   double* d_tab = nullptr;
   int n_p = 0, n_T = 0;
@@ -135,6 +131,12 @@ struct frei_ctx {
   void* comm = nullptr;
   int nranks = 1, rank = 0;
   int prefetch_depth = 0;               // 0 = automatic (FREI_PREFETCH_DEPTH overrides)
+  // Shared-bracket kernel (step table staged in LDS): used when every species shares its
+  // nodes AND the slice is small (nblocks <= shared_max_blocks, about one resident round of
+  // blocks), where each CU runs ~1 block and the per-step scalar loads would miss the K$.
+  // FREI_SHARED=0/1 forces it off/on; FREI_SHARED_MAX_BLOCKS moves the threshold.
+  int shared_mode = -1;
+  int shared_max_blocks = 1024;
   frei_allgather_fn host_ag = nullptr;  // host all-gather callback (alternative to RCCL)
   void* host_ag_user = nullptr;
   double* h_ag = nullptr;               // pinned [nranks + 1][n_steps * 4]
@@ -248,7 +250,8 @@ int build_meta(frei_ctx* c) {
     shared = shared && q.n_p == q0.n_p && q.n_T == q0.n_T && q.stride == q0.stride &&
              q.p_nodes == q0.p_nodes && q.T_nodes == q0.T_nodes;
   }
-  c->shared = FREI_SHARED_BRACKETS ? shared : 0;
+  const bool small = c->nblocks <= c->shared_max_blocks;
+  c->shared = (c->shared_mode == 1 || (c->shared_mode < 0 && small)) ? shared : 0;
   dfree(c->d_smeta);
   dfree(c->d_pmeta);
   dfree(c->d_tnodes);
@@ -487,6 +490,8 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
   c->sp.resize(n_species);
   c->nblocks = (int)((n_lam + kBlock - 1) / kBlock);
   if (const char* e = getenv("FREI_PREFETCH_DEPTH")) c->prefetch_depth = atoi(e);
+  if (const char* e = getenv("FREI_SHARED")) c->shared_mode = atoi(e) ? 1 : 0;
+  if (const char* e = getenv("FREI_SHARED_MAX_BLOCKS")) c->shared_max_blocks = atoi(e);
   auto bail = [&](int rc) {
     frei_ctx_destroy(c);
     return rc;

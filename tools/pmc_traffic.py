@@ -4,8 +4,10 @@
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts exactly half
 of the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md, HBM section), so
-HBM bytes = 2 * FETCH_SIZE + WRITE_SIZE.  Averaged over the sweep-kernel dispatches.
+HBM bytes = 2 * FETCH_SIZE + WRITE_SIZE.  Median over the sweep-kernel dispatches of each
+kernel (the timed T-P steps; excludes the rad-eq run's one full-write final emit).
 """
+import statistics
 import csv
 import json
 import sys
@@ -17,7 +19,7 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter or "sweep" not in r["Kernel_Name"]:
             continue
         vals.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]) * 1024.0)
-    return {k: sum(v) / len(v) for k, v in vals.items()}
+    return {k: statistics.median(v) for k, v in vals.items()}
 
 
 def main():
