@@ -39,6 +39,9 @@ def parse():
                     help="max T-P iterations for the iterations-to-radiative-equilibrium run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-lam", type=int, default=50_000)
+    ap.add_argument("--no-binning", action="store_true",
+                    help="skip the K6 opacity-binning measurement (rank 0)")
+    ap.add_argument("--binning-reps", type=int, default=5)
     return ap.parse_args()
 
 
@@ -95,6 +98,60 @@ def cpu_baseline(w, n_sample, steps=1):
     dt = time.perf_counter() - t0
     updates = (2 * steps + 1) * (w["p"].size - 1) * n_sample   # incl. the final emit
     return updates / dt, dt
+
+
+def binning_leg(a, device, cpu=True):
+    """K6 (opacity binning) on the C3 grid: one species' synthetic
+    DACE-like cross-section resident in HBM, binned into the reference's output shape
+    (60 x 60 (T, p) rows of 500k bins) in both modes; HIP-event kernel time, algorithmic
+    bytes per launch, CPU oracle on a bounded row sample."""
+    from frei_amd.binning import CrossSection
+    from frei_amd.workloads import binning_bytes, binning_workload
+    w = binning_workload(n_layers=a.n_layers, n_lam=a.n_lam)
+    x = CrossSection.synthetic(w["T_src"], w["p_src"], w["wl_hi"], seed=3)
+    out = {"workload": f"1 species, {w['T_src'].size} T x {w['p_src'].size} p source nodes x "
+                       f"{w['wl_hi'].size} points (0.01 cm^-1, float32) -> "
+                       f"{a.n_layers} x {a.n_layers} (T, p) rows x {a.n_lam} bins (float64)"}
+    try:
+        for mode, groupies in (("groupies", True), ("exact", False)):
+            x.bin(w["wl_bins"], w["lam"], w["T0"], w["p"], groupies=groupies, device=device,
+                  out=False)                                   # warm-up (plan + scratch)
+            x.timing(1, device)
+            for _ in range(a.binning_reps):
+                x.bin(w["wl_bins"], w["lam"], w["T0"], w["p"], groupies=groupies,
+                      device=device, out=False)
+            ms, n = x.timing(0, device)
+            acc = binning_bytes(w, groupies)
+            t = ms / n * 1e-3
+            out[mode] = {"avg_launch_ms": ms / n, "launches": n,
+                         "table_values_per_s": acc["dest_rows"] * acc["n_bins"] / t,
+                         "source_points_per_s": acc["source_rows"] * acc["points"] / t,
+                         "roofline": {"bound": "hbm", "achieved": acc["bytes"] / t / 1e9,
+                                      "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                                      "frac": acc["bytes"] / t / PEAK_HBM,
+                                      "bytes_per_launch": acc["bytes"]},
+                         "source_rows": acc["source_rows"], "dest_rows": acc["dest_rows"]}
+    finally:
+        x.release()
+    if cpu:
+        # oracle (groupies branch) on 24 random source rows of the same high-res axis and
+        # bins: binned points per second, 1 core
+        from oracle import frei_oracle as O
+        rng = np.random.default_rng(3)
+        n_rows = 24
+        rows = (10 ** rng.uniform(-3, 2, (n_rows, w["wl_hi"].size))).astype(np.float32)
+        start, end = O.bin_ranges(w["wl_hi"], w["wl_bins"])
+        t0 = time.perf_counter()
+        O.bin_groupies_rows(rows, start, end, w["wl_bins"])
+        dt = time.perf_counter() - t0
+        pts = n_rows * int(end[-1] - start[0])
+        out["cpu_baseline"] = {"value": pts / dt, "unit": "source points binned/s (groupies)",
+                               "cores": 1, "kind": "port",
+                               "sample": f"oracle bin_groupies_rows, {n_rows} source rows x "
+                                         f"{pts // n_rows} points -> {a.n_lam} bins, "
+                                         f"{dt:.2f} s"}
+        out["groupies"]["vs_cpu"] = out["groupies"]["source_points_per_s"] / (pts / dt)
+    return out
 
 
 def main():
@@ -175,6 +232,9 @@ def main():
                          f"{min(a.cpu_lam, n_lam)} lambda (evenly strided sample of the same "
                          f"grid), {S} species, 1 T-P iteration + final emit, {dt:.1f} s"}
     eng.close()
+    binning = None
+    if d.rank == 0 and not a.no_binning:
+        binning = binning_leg(a, d.local, cpu=(d.world == 1 and not a.no_cpu_baseline))
     if d.rank == 0:
         line = {
             "metric": "lambda-bin*layer flux updates/sec at 60 layers x 500k lambda",
@@ -208,6 +268,7 @@ def main():
                          "bytes_per_launch": bytes_launch,
                          "avg_launch_ms": avg_sweep_s * 1e3, "launches": n_sweeps},
             "cpu_baseline": cpu,
+            "k6_binning": binning,
         }
         print(json.dumps(line), flush=True)
 

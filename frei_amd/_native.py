@@ -17,6 +17,7 @@ _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
+_fp = ctypes.POINTER(ctypes.c_float)
 
 # int (*)(const double* send, double* recv, int64_t n, void* user)
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, _dp, _dp, _i64, _vp)
@@ -58,6 +59,18 @@ SIGNATURES = {
                                            "ALLGATHER_FN", _vp]),
     "frei_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "frei_timing_read": (ctypes.c_int, [_vp, _dp, _ip]),
+    "frei_xsec_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, _fp, ctypes.c_int,
+                                        ctypes.c_int, _i64, _dp, _dp, _dp]),
+    "frei_xsec_create_synthetic": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int,
+                                                  ctypes.c_int, ctypes.c_int, _i64, _dp, _dp,
+                                                  _dp, ctypes.c_uint64]),
+    "frei_xsec_destroy": (ctypes.c_int, [_vp]),
+    "frei_xsec_bin": (ctypes.c_int, [_vp, ctypes.c_int, _dp, _dp, _i64, _dp, ctypes.c_int, _dp,
+                                     ctypes.c_int, _dp]),
+    "frei_xsec_timing": (ctypes.c_int, [_vp, ctypes.c_int, _dp, _ip]),
+    "frei_set_table_binned": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, _dp, _dp,
+                                             _i64, _i64, _dp, ctypes.c_int, _dp,
+                                             ctypes.c_int]),
 }
 
 _lib = None
@@ -91,6 +104,12 @@ def dptr(a):
         return None
     assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"], "need C-contiguous float64"
     return a.ctypes.data_as(_dp)
+
+
+def fptr(a):
+    """Pointer to a C-contiguous float32 array."""
+    assert a.dtype == np.float32 and a.flags["C_CONTIGUOUS"], "need C-contiguous float32"
+    return a.ctypes.data_as(_fp)
 
 
 def f64(a):

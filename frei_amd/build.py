@@ -5,7 +5,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = ["csrc/frei_kernels.hip", "csrc/frei_runtime.hip"]
+SOURCES = ["csrc/frei_kernels.hip", "csrc/frei_runtime.hip", "csrc/frei_binning.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-shared", "-std=c++17"]
 
 

@@ -102,15 +102,18 @@ class Grid:
                 f"lam=[{self.lam[0]}...{self.lam[-1]}] um>")
 
     def load_opacities(self, species=None, path=None, opacities=None, client=None,
-                       force_reload=False, groupies=False, mmr=None):
+                       force_reload=False, groupies=False, mmr=None, cross_sections=None):
         """Attach opacity tables (core.py:198-231).  ``opacities`` is the reference's dict
-        of (pressure, temperature, wavelength) tables; ``mmr`` optionally overrides the mock
-        chemistry with per-species, per-layer mass mixing ratios."""
+        of (pressure, temperature, wavelength) tables; otherwise high-resolution
+        cross-sections (files at ``path`` or ``cross_sections``) are binned on the GPU
+        straight into the engine's tables (opacity.py:66-170).  ``mmr`` optionally
+        overrides the mock chemistry with per-species, per-layer mass mixing ratios."""
         if (self.opacities is None and opacities is None) or force_reload:
-            from .opacity import binned_opacity
+            from .binning import binned_opacity
             self.opacities = binned_opacity(self.init_temperatures, self.pressures,
                                             self.wl_bins, self.lam, species=species,
-                                            groupies=groupies)
+                                            path=path, groupies=groupies,
+                                            cross_sections=cross_sections, device=self.device)
         else:
             self.opacities = opacities
         self.mmr = mmr

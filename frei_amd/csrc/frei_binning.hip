@@ -1,0 +1,549 @@
+// frei_binning.hip — K6: binning of high-resolution opacity cross-sections onto a grid's
+// wavelength bins (frei/opacity.py:66-170 binned_opacity; frei/interp.py:156-307
+// groupby_bins_agg + AggregateTrapz; opacity.py:33-42 mapfunc_exact).
+//
+// Data: one species' cross-section stays resident in HBM as float32
+// [n_T][n_p][n_hi] (the opacity_dir_to_netcdf layout, opacity.py:395-483).  The host
+// side (C++, this file) builds the row-independent plan once per call — pandas.cut bin
+// ranges over the ascending high-res axis, nearest source node per target (T, p) node,
+// group coordinates and interpolation brackets — and the kernels do the row-dependent
+// streaming work:
+//   groupies (default of binned_opacity): one lane per (source row, bin) walks its bin's
+//     points in order with the reference's float32 accumulator and fans the result out
+//     to every destination (p, T) row that selected this source row (no intermediate);
+//   exact (Grid.load_opacities default): pass 1 integrates each non-empty bin for a
+//     batch of source rows per lane (the dx stream is read once per batch), pass 2
+//     interpolates linearly onto the grid wavelengths and writes every destination row.
+// Both are HBM-bound streams: float32 reads of the selected source rows + float64 writes
+// of the destination table.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/frei_hip.h"
+#include "frei_device.h"
+
+using namespace frei;
+
+struct frei_xsec {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int nT = 0, np = 0;
+  int64_t nhi = 0;
+  std::vector<double> T, p, wl;  // K, bar, µm (ascending)
+  float* d_x = nullptr;          // [nT][np][nhi]
+  double* d_hdx = nullptr;       // 0.5 * (wl[i+1] - wl[i]), exact mode (lazy)
+  double* d_scratch = nullptr;   // output of frei_xsec_bin(out = NULL)
+  size_t scratch_n = 0;
+  bool timing = false;
+  double t_ms = 0;
+  int t_n = 0;
+};
+
+namespace {
+
+constexpr int kRB = 8;  // source rows per lane in the exact-mode integration pass
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) return set_error(std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+#define TRY(expr)            \
+  do {                       \
+    int _r = (expr);         \
+    if (_r != 0) return _r;  \
+  } while (0)
+
+template <typename T>
+int dalloc(T** p, size_t n) {
+  if (n == 0) n = 1;
+  HIP_TRY(hipMalloc((void**)p, n * sizeof(T)));
+  return 0;
+}
+template <typename T>
+void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+template <typename T>
+int upload(T** d, const std::vector<T>& h, hipStream_t st) {
+  TRY(dalloc(d, h.size()));
+  if (!h.empty()) HIP_TRY(hipMemcpyAsync(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, st));
+  return 0;
+}
+
+// ------------------------------------------------------------------- kernels
+// groupies: AggregateTrapz._loop (interp.py:176-194) with dx = 1 for one (row, bin):
+// acc_f32 = f32(f64(acc_f32) + f64(f32(a_i + a_{i+1})) / 2) over consecutive pairs of the
+// bin in point order (numba promotion, float32 result array), then
+// (f64(acc) * (b_{k+1} - b_k)) * 1e-3 (opacity.py:136-139), stored to every destination
+// row of this source row.  One lane per bin loops over source rows [u0, u1) so the bin's
+// range and width are read once per lane, not once per row.
+__global__ __launch_bounds__(256) void bin_groupies_kernel(
+    const float* __restrict__ x, const int64_t* __restrict__ row_off, int U, int rows_per,
+    const int64_t* __restrict__ start, const int64_t* __restrict__ end,
+    const double* __restrict__ width, int64_t nb, const int32_t* __restrict__ fan_off,
+    const int64_t* __restrict__ fan_dst, double* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nb) return;
+  const int64_t s = start[k], e = end[k];
+  const double wk = width[k];
+  const int u0 = blockIdx.y * rows_per, u1 = min(U, u0 + rows_per);
+  for (int u = u0; u < u1; ++u) {
+    const float* __restrict__ row = x + row_off[u];
+    float acc = 0.0f;
+    if (e - s >= 2) {
+      float a = row[s];
+      int64_t i = s + 1;
+      // four loads in flight per lane; the accumulation order stays sequential
+      for (; i + 4 <= e; i += 4) {
+        const float b0 = row[i], b1 = row[i + 1], b2 = row[i + 2], b3 = row[i + 3];
+        acc = (float)((double)acc + (double)(a + b0) / 2.0);
+        acc = (float)((double)acc + (double)(b0 + b1) / 2.0);
+        acc = (float)((double)acc + (double)(b1 + b2) / 2.0);
+        acc = (float)((double)acc + (double)(b2 + b3) / 2.0);
+        a = b3;
+      }
+      for (; i < e; ++i) {
+        const float b = row[i];
+        acc = (float)((double)acc + (double)(a + b) / 2.0);
+        a = b;
+      }
+    }
+    const double v = ((double)acc * wk) * 1e-3;
+    for (int f = fan_off[u]; f < fan_off[u + 1]; ++f) out[fan_dst[f] + k] = v;
+  }
+}
+
+// exact, pass 1: xarray integrate (duck_array_ops.trapz) of one non-empty bin for kRB
+// source rows: sum_i (dx_i * 0.5) * f64(f32(y_{i+1} + y_i)) in point order, / (wl_max -
+// wl_min) (opacity.py:40-42; a single-point bin gives 0 / 0 = NaN like the reference).
+__global__ __launch_bounds__(256) void bin_exact_integrate_kernel(
+    const float* __restrict__ x, const int64_t* __restrict__ row_off, int U,
+    const int64_t* __restrict__ gstart, const int64_t* __restrict__ gend,
+    const double* __restrict__ hdx, const double* __restrict__ Dx, int64_t G,
+    double* __restrict__ res) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const int u0 = blockIdx.y * kRB;
+  const int nr = min(kRB, U - u0);
+  const int64_t s = gstart[g], e = gend[g];
+  const float* rows[kRB];
+  double acc[kRB];
+  float prev[kRB];
+#pragma unroll
+  for (int r = 0; r < kRB; ++r) {
+    rows[r] = x + row_off[u0 + (r < nr ? r : 0)];
+    acc[r] = 0.0;
+    prev[r] = rows[r][s];
+  }
+  for (int64_t i = s; i + 1 < e; ++i) {
+    const double h = hdx[i];
+#pragma unroll
+    for (int r = 0; r < kRB; ++r) {
+      const float b = rows[r][i + 1];
+      acc[r] = acc[r] + h * (double)(b + prev[r]);
+      prev[r] = b;
+    }
+  }
+  const double d = Dx[g];
+#pragma unroll
+  for (int r = 0; r < kRB; ++r)
+    if (r < nr) res[(int64_t)(u0 + r) * G + g] = acc[r] / d;
+}
+
+// exact, pass 2: scipy interp1d(kind='linear', fill_value='extrapolate') onto the grid
+// wavelengths, slope = (y_hi - y_lo) / (x_hi - x_lo), y = slope * (x - x_lo) + y_lo.
+// One lane per wavelength loops over destination rows [d0, d1) (source row dst_src[d]),
+// so the per-wavelength bracket is read once per lane.
+__global__ __launch_bounds__(256) void bin_exact_expand_kernel(
+    const double* __restrict__ res, int64_t G, const int32_t* __restrict__ dst_src, int D,
+    int rows_per, const int64_t* __restrict__ dst_off, const int32_t* __restrict__ lo,
+    const double* __restrict__ xlo, const double* __restrict__ xhi,
+    const double* __restrict__ lam, int64_t n, double* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int32_t l = lo[j];
+  const double dxj = xhi[j] - xlo[j], t = lam[j] - xlo[j];
+  const int d0 = blockIdx.y * rows_per, d1 = min(D, d0 + rows_per);
+  for (int d = d0; d < d1; ++d) {
+    const double* __restrict__ y = res + (int64_t)dst_src[d] * G;
+    const double ylo = y[l], yhi = y[l + 1];
+    const double slope = (yhi - ylo) / dxj;
+    out[dst_off[d] + j] = slope * t + ylo;
+  }
+}
+
+// Synthetic DACE-like line forest for benchmarks (no host copy of n_T*n_p*n_hi values):
+// 10^(-1.5 + 0.9 sin(1.7 ln wl) + 3 u^8) * (T / 1000)^0.5 * p^0.05, u = hash(i, seed).
+__global__ void gen_xsec_kernel(float* __restrict__ x, int nT, int np, int64_t nhi,
+                                const double* __restrict__ T, const double* __restrict__ p,
+                                const double* __restrict__ wl, uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nhi) return;
+  uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull ^ seed;
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  const double u = (double)(h >> 11) * (1.0 / 9007199254740992.0);
+  const double u2 = u * u, u4 = u2 * u2;
+  const double base = pow(10.0, -1.5 + 0.9 * sin(1.7 * log(wl[i])) + 3.0 * u4 * u4);
+  for (int a = 0; a < nT; ++a)
+    for (int b = 0; b < np; ++b)
+      x[((int64_t)a * np + b) * nhi + i] =
+          (float)(base * sqrt(T[a] / 1000.0) * pow(p[b], 0.05));
+}
+
+// ------------------------------------------------------------------- host plan
+// scipy interp1d 'nearest' after xarray sortby: midpoints x[i]/2 + x[i+1]/2, searchsorted
+// side='left', clipped (opacity.py:26-29 interp_kwargs, fill_value='extrapolate').
+std::vector<int> nearest_index(const std::vector<double>& nodes, const double* t, int n) {
+  std::vector<int> order(nodes.size());
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return nodes[a] < nodes[b]; });
+  std::vector<double> bds;
+  for (size_t i = 0; i + 1 < order.size(); ++i)
+    bds.push_back(nodes[order[i + 1]] / 2.0 + nodes[order[i]] / 2.0);
+  std::vector<int> out(n);
+  for (int j = 0; j < n; ++j) {
+    const int64_t k = std::lower_bound(bds.begin(), bds.end(), t[j]) - bds.begin();
+    out[j] = order[std::min<int64_t>(k, (int64_t)order.size() - 1)];
+  }
+  return out;
+}
+
+// numpy pairwise summation (np.mean of the group wavelengths, opacity.py:42).
+double pairwise_sum(const double* a, int64_t n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int64_t i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  if (n <= 128) {
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int64_t i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  }
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  return pairwise_sum(a, n2) + pairwise_sum(a + n2, n - n2);
+}
+
+// Rows handled per lane: enough workgroups to fill 256 CUs (~8 per CU) without
+// re-reading the per-wavelength plan once per row.
+int rows_per_lane(int64_t n, int rows) {
+  const int64_t blocks_x = (n + 255) / 256;
+  const int64_t want_y = std::max<int64_t>(1, (2048 + blocks_x - 1) / blocks_x);
+  const int64_t per = (rows + want_y - 1) / want_y;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(per, rows));
+}
+
+struct Dest {
+  // destination rows: (p index kp, T index kt) -> element offset in the output
+  int n_p = 0, n_T = 0;
+  std::vector<int64_t> off;  // [n_p * n_T] row-major over (kp, kt)
+};
+
+int check_ascending(const double* a, int64_t n, const char* what) {
+  for (int64_t i = 0; i + 1 < n; ++i)
+    if (!(a[i + 1] > a[i])) return set_error(std::string(what) + " must be strictly ascending");
+  return 0;
+}
+
+// The whole binning of one species into device buffer `out` (rows at dest.off).
+int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, int64_t n_bins,
+             int64_t lam_lo, int64_t n_out, const double* T_t, const double* p_t,
+             const Dest& dest, double* d_out) {
+  if (mode != FREI_BIN_GROUPIES && mode != FREI_BIN_EXACT) return set_error("unknown binning mode");
+  if (n_bins < 1 || lam_lo < 0 || n_out < 1 || lam_lo + n_out > n_bins)
+    return set_error("wavelength slice outside the grid");
+  TRY(check_ascending(wl_bins, n_bins + 1, "wl_bins"));
+  hipStream_t st = x->stream;
+  const std::vector<double>& wl = x->wl;
+  // pandas.cut(right=True) ranges on the cropped axis b_0 < x < b_last
+  std::vector<int64_t> start(n_bins), end(n_bins);
+  for (int64_t k = 0; k < n_bins; ++k) {
+    start[k] = std::upper_bound(wl.begin(), wl.end(), wl_bins[k]) - wl.begin();
+    end[k] = (k + 1 < n_bins ? std::upper_bound(wl.begin(), wl.end(), wl_bins[k + 1])
+                             : std::lower_bound(wl.begin(), wl.end(), wl_bins[k + 1])) -
+             wl.begin();
+    end[k] = std::max(end[k], start[k]);
+  }
+  // nearest source nodes and the unique source rows they select
+  const std::vector<int> ti = nearest_index(x->T, T_t, dest.n_T);
+  const std::vector<int> pi = nearest_index(x->p, p_t, dest.n_p);
+  std::map<int64_t, int> uid;  // source row -> unique index (ascending source order)
+  for (int kp = 0; kp < dest.n_p; ++kp)
+    for (int kt = 0; kt < dest.n_T; ++kt) uid[(int64_t)ti[kt] * x->np + pi[kp]] = 0;
+  std::vector<int64_t> row_off;
+  for (auto& kv : uid) {
+    kv.second = (int)row_off.size();
+    row_off.push_back(kv.first * x->nhi);
+  }
+  const int U = (int)row_off.size();
+  std::vector<int32_t> dst_src(dest.off.size());
+  for (int kp = 0; kp < dest.n_p; ++kp)
+    for (int kt = 0; kt < dest.n_T; ++kt)
+      dst_src[(size_t)kp * dest.n_T + kt] = uid[(int64_t)ti[kt] * x->np + pi[kp]];
+
+  std::vector<void*> tmp;
+  auto cleanup = [&]() {
+    (void)hipStreamSynchronize(st);
+    for (void* q : tmp) (void)hipFree(q);
+  };
+  int64_t* d_row = nullptr;
+  if (int rc = upload(&d_row, row_off, st)) return cleanup(), rc;
+  tmp.push_back(d_row);
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  if (x->timing)
+    for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+  int rc = 0;
+  if (mode == FREI_BIN_GROUPIES) {
+    // bins [lam_lo, lam_lo + n_out) map 1:1 to output wavelengths
+    std::vector<int64_t> s(start.begin() + lam_lo, start.begin() + lam_lo + n_out),
+        e(end.begin() + lam_lo, end.begin() + lam_lo + n_out);
+    std::vector<double> w(n_out);
+    for (int64_t k = 0; k < n_out; ++k) w[k] = wl_bins[lam_lo + k + 1] - wl_bins[lam_lo + k];
+    std::vector<int32_t> fan_off(U + 1, 0);
+    for (int32_t q : dst_src) fan_off[q + 1]++;
+    for (int u = 0; u < U; ++u) fan_off[u + 1] += fan_off[u];
+    std::vector<int64_t> fan_dst(dst_src.size());
+    std::vector<int32_t> fill(fan_off.begin(), fan_off.end() - 1);
+    for (size_t d = 0; d < dst_src.size(); ++d) fan_dst[fill[dst_src[d]]++] = dest.off[d];
+    int64_t *d_s = nullptr, *d_e = nullptr, *d_fd = nullptr;
+    double* d_w = nullptr;
+    int32_t* d_fo = nullptr;
+    if ((rc = upload(&d_s, s, st)) || (tmp.push_back(d_s), rc = upload(&d_e, e, st)) ||
+        (tmp.push_back(d_e), rc = upload(&d_w, w, st)) ||
+        (tmp.push_back(d_w), rc = upload(&d_fo, fan_off, st)) ||
+        (tmp.push_back(d_fo), rc = upload(&d_fd, fan_dst, st)))
+      return cleanup(), rc;
+    tmp.push_back(d_fd);
+    const int rows_per = rows_per_lane(n_out, U);
+    dim3 grid((unsigned)((n_out + 255) / 256), (unsigned)((U + rows_per - 1) / rows_per));
+    if (x->timing) HIP_TRY(hipEventRecord(ev[0], st));
+    bin_groupies_kernel<<<grid, 256, 0, st>>>(x->d_x, d_row, U, rows_per, d_s, d_e, d_w, n_out,
+                                              d_fo, d_fd, d_out);
+  } else {
+    // non-empty groups (xarray groupby_bins drops empty bins) and their coordinates
+    std::vector<int64_t> gs, ge;
+    std::vector<double> xc, Dx;
+    for (int64_t k = 0; k < n_bins; ++k)
+      if (end[k] > start[k]) {
+        gs.push_back(start[k]);
+        ge.push_back(end[k]);
+        xc.push_back(pairwise_sum(wl.data() + start[k], end[k] - start[k]) /
+                     (double)(end[k] - start[k]));
+        Dx.push_back(wl[end[k] - 1] - wl[start[k]]);
+      }
+    const int64_t Gall = (int64_t)xc.size();
+    if (Gall < 2) return cleanup(), set_error("x and y arrays must have at least 2 entries");
+    // interval of each output wavelength: clip(searchsorted(x, lam), 1, G - 1)
+    std::vector<int64_t> hi(n_out);
+    for (int64_t j = 0; j < n_out; ++j) {
+      const int64_t h = std::lower_bound(xc.begin(), xc.end(), lam[lam_lo + j]) - xc.begin();
+      hi[j] = std::min<int64_t>(std::max<int64_t>(h, 1), Gall - 1);
+    }
+    const int64_t g0 = *std::min_element(hi.begin(), hi.end()) - 1;
+    const int64_t g1 = *std::max_element(hi.begin(), hi.end()) + 1;  // groups [g0, g1)
+    const int64_t G = g1 - g0;
+    std::vector<int64_t> s(gs.begin() + g0, gs.begin() + g1), e(ge.begin() + g0, ge.begin() + g1);
+    std::vector<double> dx(Dx.begin() + g0, Dx.begin() + g1);
+    std::vector<int32_t> lo(n_out);
+    std::vector<double> xlo(n_out), xhi(n_out), lamv(lam + lam_lo, lam + lam_lo + n_out);
+    for (int64_t j = 0; j < n_out; ++j) {
+      lo[j] = (int32_t)(hi[j] - 1 - g0);
+      xlo[j] = xc[hi[j] - 1];
+      xhi[j] = xc[hi[j]];
+    }
+    if (!x->d_hdx) {
+      std::vector<double> h(std::max<int64_t>(x->nhi - 1, 1));
+      for (int64_t i = 0; i + 1 < x->nhi; ++i) h[i] = (wl[i + 1] - wl[i]) * 0.5;
+      if ((rc = upload(&x->d_hdx, h, st))) return cleanup(), rc;
+    }
+    int64_t *d_s = nullptr, *d_e = nullptr, *d_do = nullptr;
+    double *d_D = nullptr, *d_res = nullptr, *d_xlo = nullptr, *d_xhi = nullptr,
+           *d_lam = nullptr;
+    int32_t *d_lo = nullptr, *d_ds = nullptr;
+    if ((rc = upload(&d_s, s, st)) || (tmp.push_back(d_s), rc = upload(&d_e, e, st)) ||
+        (tmp.push_back(d_e), rc = upload(&d_D, dx, st)) ||
+        (tmp.push_back(d_D), rc = dalloc(&d_res, (size_t)U * G)) ||
+        (tmp.push_back(d_res), rc = upload(&d_lo, lo, st)) ||
+        (tmp.push_back(d_lo), rc = upload(&d_xlo, xlo, st)) ||
+        (tmp.push_back(d_xlo), rc = upload(&d_xhi, xhi, st)) ||
+        (tmp.push_back(d_xhi), rc = upload(&d_lam, lamv, st)) ||
+        (tmp.push_back(d_lam), rc = upload(&d_ds, dst_src, st)) ||
+        (tmp.push_back(d_ds), rc = upload(&d_do, dest.off, st)))
+      return cleanup(), rc;
+    tmp.push_back(d_do);
+    dim3 g1d((unsigned)((G + 255) / 256), (unsigned)((U + kRB - 1) / kRB));
+    if (x->timing) HIP_TRY(hipEventRecord(ev[0], st));
+    bin_exact_integrate_kernel<<<g1d, 256, 0, st>>>(x->d_x, d_row, U, d_s, d_e, x->d_hdx, d_D,
+                                                    G, d_res);
+    const int D = (int)dst_src.size();
+    const int dper = rows_per_lane(n_out, D);
+    dim3 g2d((unsigned)((n_out + 255) / 256), (unsigned)((D + dper - 1) / dper));
+    bin_exact_expand_kernel<<<g2d, 256, 0, st>>>(d_res, G, d_ds, D, dper, d_do, d_lo, d_xlo,
+                                                 d_xhi, d_lam, n_out, d_out);
+  }
+  if (hipGetLastError() != hipSuccess) return cleanup(), set_error("binning kernel launch failed");
+  if (x->timing) {
+    HIP_TRY(hipEventRecord(ev[1], st));
+    HIP_TRY(hipEventSynchronize(ev[1]));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    x->t_ms += ms;
+    x->t_n += 1;
+    for (auto e : ev) (void)hipEventDestroy(e);
+  }
+  if (hipStreamSynchronize(st) != hipSuccess) return cleanup(), set_error("binning kernels failed");
+  cleanup();
+  return 0;
+}
+
+}  // namespace
+
+namespace frei {
+// frei_set_table_binned (frei_runtime.hip): bin species into a context table whose rows for
+// destination node (kp, kt) start at row_off[kp * n_T + kt].
+int bin_into_table(frei_xsec* x, int mode, const double* wl_bins, const double* lam,
+                   int64_t n_bins, int64_t lam_lo, int64_t n_out, const double* T_t, int n_T,
+                   const double* p_t, int n_p, const int64_t* row_off, double* d_tab,
+                   int device) {
+  if (!x) return set_error("null cross-section");
+  if (x->device != device) return set_error("cross-section and context are on different devices");
+  Dest d;
+  d.n_p = n_p;
+  d.n_T = n_T;
+  d.off.assign(row_off, row_off + (size_t)n_p * n_T);
+  HIP_TRY(hipSetDevice(x->device));
+  return bin_into(x, mode, wl_bins, lam, n_bins, lam_lo, n_out, T_t, p_t, d, d_tab);
+}
+}  // namespace frei
+
+// ==================================================================== C ABI
+extern "C" {
+
+static int xsec_alloc(frei_xsec** out, int device, int n_T, int n_p, int64_t n_hi,
+                      const double* T_nodes, const double* p_nodes, const double* wl_hi) {
+  if (!out || !T_nodes || !p_nodes || !wl_hi) return set_error("null argument");
+  *out = nullptr;
+  if (n_T < 1 || n_p < 1 || n_hi < 2) return set_error("empty cross-section grid");
+  TRY(check_ascending(wl_hi, n_hi, "high-resolution wavelengths"));
+  frei_xsec* x = new frei_xsec();
+  x->device = device;
+  x->nT = n_T;
+  x->np = n_p;
+  x->nhi = n_hi;
+  x->T.assign(T_nodes, T_nodes + n_T);
+  x->p.assign(p_nodes, p_nodes + n_p);
+  x->wl.assign(wl_hi, wl_hi + n_hi);
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void**)&x->d_x, (size_t)n_T * n_p * n_hi * sizeof(float)) != hipSuccess) {
+    frei_xsec_destroy(x);
+    return set_error("frei_xsec: device allocation failed");
+  }
+  *out = x;
+  return 0;
+}
+
+int frei_xsec_create(frei_xsec** out, int device, const float* values, int n_T, int n_p,
+                     int64_t n_hi, const double* T_nodes, const double* p_nodes,
+                     const double* wl_hi) {
+  if (!values) return set_error("null argument");
+  TRY(xsec_alloc(out, device, n_T, n_p, n_hi, T_nodes, p_nodes, wl_hi));
+  frei_xsec* x = *out;
+  if (hipMemcpy(x->d_x, values, (size_t)n_T * n_p * n_hi * sizeof(float),
+                hipMemcpyHostToDevice) != hipSuccess) {
+    frei_xsec_destroy(x);
+    *out = nullptr;
+    return set_error("frei_xsec_create: host-to-device copy failed");
+  }
+  return 0;
+}
+
+int frei_xsec_create_synthetic(frei_xsec** out, int device, int n_T, int n_p, int64_t n_hi,
+                               const double* T_nodes, const double* p_nodes,
+                               const double* wl_hi, uint64_t seed) {
+  TRY(xsec_alloc(out, device, n_T, n_p, n_hi, T_nodes, p_nodes, wl_hi));
+  frei_xsec* x = *out;
+  double *d_T = nullptr, *d_p = nullptr, *d_wl = nullptr;
+  int rc = 0;
+  if ((rc = upload(&d_T, x->T, x->stream)) || (rc = upload(&d_p, x->p, x->stream)) ||
+      (rc = upload(&d_wl, x->wl, x->stream))) {
+    dfree(d_T), dfree(d_p), dfree(d_wl);
+    frei_xsec_destroy(x);
+    *out = nullptr;
+    return rc;
+  }
+  gen_xsec_kernel<<<(unsigned)((n_hi + 255) / 256), 256, 0, x->stream>>>(x->d_x, n_T, n_p, n_hi,
+                                                                        d_T, d_p, d_wl, seed);
+  const bool ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(x->stream) == hipSuccess;
+  dfree(d_T), dfree(d_p), dfree(d_wl);
+  if (!ok) {
+    frei_xsec_destroy(x);
+    *out = nullptr;
+    return set_error("frei_xsec_create_synthetic: generation failed");
+  }
+  return 0;
+}
+
+int frei_xsec_destroy(frei_xsec* x) {
+  if (!x) return 0;
+  (void)hipSetDevice(x->device);
+  if (x->stream) (void)hipStreamSynchronize(x->stream);
+  dfree(x->d_x);
+  dfree(x->d_hdx);
+  dfree(x->d_scratch);
+  if (x->stream) (void)hipStreamDestroy(x->stream);
+  delete x;
+  return 0;
+}
+
+int frei_xsec_bin(frei_xsec* x, int mode, const double* wl_bins, const double* lam,
+                  int64_t n_bins, const double* T_nodes, int n_T, const double* p_nodes,
+                  int n_p, double* out) {
+  if (!x || !wl_bins || !lam || !T_nodes || !p_nodes) return set_error("null argument");
+  if (n_T < 1 || n_p < 1) return set_error("need at least one target (T, p) node");
+  HIP_TRY(hipSetDevice(x->device));
+  const size_t total = (size_t)n_p * n_T * n_bins;
+  if (x->scratch_n < total) {
+    dfree(x->d_scratch);
+    x->scratch_n = 0;
+    TRY(dalloc(&x->d_scratch, total));
+    x->scratch_n = total;
+  }
+  Dest d;
+  d.n_p = n_p;
+  d.n_T = n_T;
+  d.off.resize((size_t)n_p * n_T);
+  for (size_t r = 0; r < d.off.size(); ++r) d.off[r] = (int64_t)r * n_bins;
+  TRY(bin_into(x, mode, wl_bins, lam, n_bins, 0, n_bins, T_nodes, p_nodes, d, x->d_scratch));
+  if (out) HIP_TRY(hipMemcpy(out, x->d_scratch, total * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int frei_xsec_timing(frei_xsec* x, int on, double* total_ms, int* n_calls) {
+  if (!x) return set_error("null argument");
+  if (total_ms) *total_ms = x->t_ms;
+  if (n_calls) *n_calls = x->t_n;
+  if (on >= 0) {
+    x->timing = on != 0;
+    x->t_ms = 0;
+    x->t_n = 0;
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <string>
 
 namespace frei {
 
@@ -248,5 +249,16 @@ void launch_gen_table(double* tab, const double* base, const double* fp, const d
                       int n_p, int n_T, int64_t n_lam, int64_t stride, double lo, double hi,
                       hipStream_t st);
 void launch_fill(double* x, int64_t n, double v, hipStream_t st);
+
+// Error reporting shared by the runtime and the binning module (frei_last_error()).
+int set_error(const std::string& msg);
+}  // namespace frei
+struct frei_xsec;
+namespace frei {
+// K6 (frei_binning.hip): bin one species into table rows d_tab + row_off[kp * n_T + kt].
+int bin_into_table(frei_xsec* x, int mode, const double* wl_bins, const double* lam,
+                   int64_t n_bins, int64_t lam_lo, int64_t n_out, const double* T_t, int n_T,
+                   const double* p_t, int n_p, const int64_t* row_off, double* d_tab,
+                   int device);
 
 }  // namespace frei

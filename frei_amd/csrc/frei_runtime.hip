@@ -27,6 +27,14 @@ int fail(const std::string& msg) {
   return -1;
 }
 
+}  // namespace
+
+namespace frei {
+int set_error(const std::string& msg) { return fail(msg); }
+}  // namespace frei
+
+namespace {
+
 #define HIP_TRY(expr)                                                              \
   do {                                                                             \
     hipError_t _e = (expr);                                                        \
@@ -683,6 +691,27 @@ int frei_set_table_separable(frei_ctx* c, int s, const double* base, const doubl
   dfree(d_base);
   dfree(d_fp);
   dfree(d_fT);
+  return scan_nan(c, s);
+}
+
+int frei_set_table_binned(frei_ctx* c, int s, frei_xsec* x, int mode, const double* wl_bins,
+                          const double* lam, int64_t n_bins, int64_t lam_lo,
+                          const double* T_nodes, int n_T, const double* p_nodes, int n_p) {
+  if (!c || !x || !wl_bins || !lam || !T_nodes || !p_nodes) return fail("null argument");
+  TRY(set_device(c));
+  std::vector<double> p_cgs(n_p > 0 ? n_p : 0);
+  for (int k = 0; k < n_p; ++k) p_cgs[k] = p_nodes[k] * 1e6;  // bar -> dyn cm^-2
+  TRY(set_table_common(c, s, p_cgs.data(), n_p, T_nodes, n_T));
+  // destination row of node (kp, kt): the T axis is stored ascending
+  const std::vector<int32_t> perm = t_order(T_nodes, n_T);
+  std::vector<int32_t> rank(n_T);
+  for (int t = 0; t < n_T; ++t) rank[perm[t]] = t;
+  std::vector<int64_t> row_off((size_t)n_p * n_T);
+  for (int kp = 0; kp < n_p; ++kp)
+    for (int kt = 0; kt < n_T; ++kt)
+      row_off[(size_t)kp * n_T + kt] = ((int64_t)kp * n_T + rank[kt]) * c->sp[s].stride;
+  TRY(bin_into_table(x, mode, wl_bins, lam, n_bins, lam_lo, c->nlam, T_nodes, n_T, p_nodes,
+                     n_p, row_off.data(), c->sp[s].d_tab, c->device));
   return scan_nan(c, s);
 }
 

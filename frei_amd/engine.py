@@ -12,6 +12,7 @@ import ctypes
 import numpy as np
 
 from . import _native as N
+from .binning import BinnedTable
 from .chemistry import chemistry
 from .constants import BAR, C, H, K_B, M_BAR_DEFAULT, UM
 from .opacity import SeparableTable, sigma_scattering
@@ -137,6 +138,14 @@ class Engine:
         lib = N.lib()
         p, T = _table_arrays(tab)
         p_cgs, T = N.f64(p * BAR), N.f64(T)
+        if isinstance(tab, BinnedTable):
+            if tab.wavelength.size != self.lam_um.size:
+                raise ValueError("binned table wavelengths must match the grid")
+            N.check(lib.frei_set_table_binned(
+                self._ctx, s, tab.xsec.handle(self.device), tab.mode, N.dptr(tab.wl_bins),
+                N.dptr(tab.wavelength), tab.wavelength.size, self.lo, N.dptr(tab.temperature),
+                tab.temperature.size, N.dptr(tab.pressure), tab.pressure.size))
+            return
         if isinstance(tab, SeparableTable):
             N.check(lib.frei_set_table_separable(
                 self._ctx, s, N.dptr(N.f64(tab.base[sl])), N.dptr(N.f64(tab.fp)),

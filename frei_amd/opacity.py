@@ -133,8 +133,10 @@ def load_example_opacity(grid, seed=42, scale_factor=20):
     return {"1H2-16O": OpacityTable(vals, p, T, lam).drop_duplicates("temperature")}
 
 
-def binned_opacity(*args, **kwargs):
-    """Binning of high-resolution DACE cross-sections (opacity.py:66-170) is the next
-    component of SURVEY.md §8(f) and not part of this round's engine."""
-    raise NotImplementedError("binned_opacity: pass precomputed tables via "
-                              "Grid.load_opacities(opacities=...) (SURVEY.md §8(f) #1)")
+def binned_opacity(temperatures, pressures, wl_bins, lam, groupies=True, species=None,
+                   path=None, **kwargs):
+    """Bin high-resolution cross-sections onto ``lam`` (opacity.py:66-170) on the GPU;
+    see :func:`frei_amd.binning.binned_opacity`."""
+    from .binning import binned_opacity as _bo
+    return _bo(temperatures, pressures, wl_bins, lam, groupies=groupies, species=species,
+               path=path, **kwargs)

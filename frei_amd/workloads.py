@@ -65,3 +65,49 @@ def bytes_per_update(n_species, write_dtau=False, live_only=False):
     Inside the T-P loop (live_only) one of the two flux rows per step is a dead store that
     the engine skips, so 8 + 8 + 16 S."""
     return 8 + (8 if live_only else 16) + 16 * n_species + (8 if write_dtau else 0)
+
+
+def binning_workload(n_layers=60, n_lam=500_000, T_ref=1500.0, spacing_cm=0.01,
+                     n_T_src=20, n_p_src=12):
+    """K6 benchmark: one species' DACE-like cross-section (float32, wavenumber spacing
+    ``spacing_cm`` cm^-1 over 1000-20000 cm^-1, i.e. 0.5-10 µm; ``n_T_src`` x ``n_p_src``
+    nodes 500-4300 K x 1e-6-100 bar) binned onto the C3 grid with the reference's output
+    shape: every (grid T, grid p) node (n_layers x n_layers rows of n_lam bins)."""
+    lam, wl_bins, _ = wavelength_grid(0.5, 10, n_lam)
+    p = pressure_grid(n_layers, -6, np.log10(200))
+    T0 = temperature_grid(p, T_ref, 0.1, 0.1)
+    wlen = np.arange(1000, 20000, spacing_cm)
+    wl_hi = (1 / wlen / 1e-4)[1:][::-1]                 # opacity.py:409-414
+    T_src = np.linspace(500.0, 4300.0, n_T_src)
+    p_src = np.logspace(-6, 2, n_p_src)
+    return dict(lam=lam, wl_bins=wl_bins, p=p, T0=T0, wl_hi=wl_hi, T_src=T_src, p_src=p_src)
+
+
+def nearest_index(nodes, targets):
+    """Nearest-node selection of the binning plan (interp 'nearest', ties to the lower node,
+    extrapolating): for accounting the rows a binning launch reads."""
+    nodes = np.asarray(nodes, dtype=float)
+    order = np.argsort(nodes, kind="stable")
+    x = nodes[order]
+    if x.size == 1:
+        return np.full(np.size(targets), order[0])
+    h = x / 2.0
+    return order[np.clip(np.searchsorted(h[1:] + h[:-1], targets, side="left"), 0, x.size - 1)]
+
+
+def binning_bytes(w, groupies=True):
+    """Algorithmic HBM bytes of one binning launch: every selected source row read once over
+    the binned wavelength range (float32), every destination table row written once
+    (float64), the per-bin plan (start, end, width: 24 B per bin) read once; the exact
+    mode also reads the float64 dx stream once."""
+    wl, b = w["wl_hi"], w["wl_bins"]
+    lo = np.searchsorted(wl, b[0], side="right")
+    hi = np.searchsorted(wl, b[-1], side="left")
+    P = int(hi - lo)
+    U = len({(t, q) for t in nearest_index(w["T_src"], w["T0"])
+             for q in nearest_index(w["p_src"], w["p"])})
+    D = w["T0"].size * w["p"].size
+    n = w["lam"].size
+    reads = U * P * 4 + 24 * n + (0 if groupies else 8 * P)
+    writes = D * n * 8
+    return dict(bytes=reads + writes, source_rows=U, points=P, dest_rows=D, n_bins=n)

@@ -12,6 +12,9 @@
  *   frei_run                frei/core.py:233-338       Grid.emission_spectrum(...)
  *   frei_set_table*         frei/core.py:198-231       Grid.load_opacities(opacities=...)
  *   frei_set_grid           frei/core.py:113-188,48-55 Grid(...) + F_TOA(...)
+ *   frei_xsec_bin           frei/opacity.py:66-170     binned_opacity(...) (one species)
+ *                           frei/interp.py:156-307     groupby_bins_agg / AggregateTrapz
+ *   frei_set_table_binned   frei/core.py:198-231       Grid.load_opacities(species, path)
  *
  * Conventions (all plain pointers and sizes, no framework types):
  *   - Units are cgs: wavelength cm, pressure dyn cm^-2, T K, flux erg s^-1 cm^-3,
@@ -147,6 +150,50 @@ int frei_comm_init_host(frei_ctx* ctx, int nranks, int rank, frei_allgather_fn f
  * launch while enabled): total milliseconds and number of timed launches. */
 int frei_timing_enable(frei_ctx* ctx, int on);
 int frei_timing_read(frei_ctx* ctx, double* total_ms, int* n_launches);
+
+/*
+ * Opacity binning (opacity.py:66-170).  A frei_xsec is one species' high-resolution
+ * cross-section resident in HBM, in the opacity_dir_to_netcdf layout (opacity.py:395-483):
+ * values[n_T][n_p][n_hi] float32 on nodes T_nodes (K) x p_nodes (bar), wavelengths
+ * wl_hi[n_hi] (µm, strictly ascending).
+ */
+typedef struct frei_xsec frei_xsec;
+enum { FREI_BIN_GROUPIES = 0, FREI_BIN_EXACT = 1 };
+
+int frei_xsec_create(frei_xsec** out, int device, const float* values, int n_T, int n_p,
+                     int64_t n_hi, const double* T_nodes, const double* p_nodes,
+                     const double* wl_hi);
+/* Synthetic line forest generated on the device (benchmarks; no host copy). */
+int frei_xsec_create_synthetic(frei_xsec** out, int device, int n_T, int n_p, int64_t n_hi,
+                               const double* T_nodes, const double* p_nodes,
+                               const double* wl_hi, uint64_t seed);
+int frei_xsec_destroy(frei_xsec* x);
+/*
+ * binned_opacity for this species onto a grid: bins wl_bins[n_bins+1] (µm, ascending) with
+ * centres lam[n_bins] (µm).  Target nodes T_nodes[n_T] (K) x p_nodes[n_p] (bar) each take
+ * the nearest source node (xarray interp 'nearest', extrapolating; opacity.py:26-29).
+ *   mode FREI_BIN_GROUPIES (binned_opacity default, opacity.py:126-146): per bin the
+ *     reference's float32 unit-step trapezoid (interp.py:176-194) x bin width x 1e-3;
+ *   mode FREI_BIN_EXACT (Grid.load_opacities default, opacity.py:148-167): per non-empty
+ *     bin the trapezoid integral / bin span (NaN for single-point bins) at the bin's mean
+ *     wavelength, then linear interpolation/extrapolation onto lam.
+ * out[n_p][n_T][n_bins] float64 on the host (NULL: leave the result on the device, for
+ * timing).
+ */
+int frei_xsec_bin(frei_xsec* x, int mode, const double* wl_bins, const double* lam,
+                  int64_t n_bins, const double* T_nodes, int n_T, const double* p_nodes,
+                  int n_p, double* out);
+/* HIP-event timing of the binning kernels: returns the accumulated milliseconds and calls
+ * since the last reset; on = 1/0 enables/disables and resets, on = -1 only reads. */
+int frei_xsec_timing(frei_xsec* x, int on, double* total_ms, int* n_calls);
+/*
+ * Same binning, written straight into species s of a context (no host round trip): the
+ * context's wavelength slice is [lam_lo, lam_lo + n_lam) of the global grid
+ * (wl_bins[n_bins+1], lam[n_bins]); the table gets nodes p_nodes (bar) x T_nodes (K).
+ */
+int frei_set_table_binned(frei_ctx* ctx, int s, frei_xsec* x, int mode, const double* wl_bins,
+                          const double* lam, int64_t n_bins, int64_t lam_lo,
+                          const double* T_nodes, int n_T, const double* p_nodes, int n_p);
 
 #ifdef __cplusplus
 }

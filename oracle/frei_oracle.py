@@ -485,3 +485,121 @@ class SeparableValues:
         fp = self.fp[pidx]
         return np.clip((fp[:, None] * self.fT[None, :])[:, :, None] * self.base[None, None, :],
                        self.lo, self.hi)
+
+
+# ----------------------------------------------------------------- opacity binning (§8(f) #1)
+# binned_opacity (opacity.py:66-170): high-resolution cross-sections in the
+# opacity_dir_to_netcdf layout (opacity.py:395-483: float32 (temperature, pressure,
+# wavelength), wavelength µm ascending) binned onto a Grid's wavelength bins, then the
+# nearest source (T, p) node is taken for every target node.  Pinned by
+# tests/golden/binning.npz (the reference's own binned_opacity + interp.py, run under
+# tests/golden/binharness.py stand-ins for numba/numpy_groupies/xarray; real pandas).
+def nearest_index(nodes, targets):
+    """xarray interp(method='nearest', fill_value='extrapolate') index selection: sortby,
+    then scipy interp1d 'nearest' — midpoints x[i]/2 + x[i+1]/2, searchsorted side='left'
+    (a target exactly on a midpoint takes the lower node), clipped to the end nodes."""
+    nodes = np.asarray(nodes, dtype=float)
+    order = np.argsort(nodes, kind="stable")
+    x = nodes[order]
+    if x.size == 1:
+        return np.zeros(np.size(targets), dtype=np.int64) + order[0]
+    h = x / 2.0
+    bds = h[1:] + h[:-1]
+    idx = np.clip(np.searchsorted(bds, np.asarray(targets, dtype=float), side="left"),
+                  0, x.size - 1)
+    return order[idx]
+
+
+def bin_ranges(wl_hi, wl_bins):
+    """pandas.cut(right=True) bin membership on the cropped axis
+    wl_bins.min() < x < wl_bins.max() (opacity.py:131-135, interp.py:289): point ranges
+    [start_k, end_k) of bin k = (b_k, b_{k+1}] for an ascending high-res axis."""
+    wl_hi = np.asarray(wl_hi, dtype=float)
+    b = np.asarray(wl_bins, dtype=float)
+    if np.any(np.diff(wl_hi) <= 0) or np.any(np.diff(b) <= 0):
+        raise ValueError("wavelengths and bin edges must be strictly ascending")
+    start = np.searchsorted(wl_hi, b[:-1], side="right")
+    end = np.searchsorted(wl_hi, b[1:], side="right")
+    end[-1] = np.searchsorted(wl_hi, b[-1], side="left")   # x < wl_bins.max() (cropping)
+    return start.astype(np.int64), np.maximum(end, start).astype(np.int64)
+
+
+def bin_groupies_rows(rows_f32, start, end, wl_bins):
+    """groupby_bins_agg(..., func=np.trapz) * (wl_bins[1:] - wl_bins[:-1]) * 1e-3
+    (opacity.py:136-139; interp.py:156-207, 246-307).  Per row and bin: the pair rule of
+    AggregateTrapz._loop — consecutive points i, i+1 in the same bin add
+    ((a_i + a_{i+1}) / 2) * dx with dx = 1 (_binned_agg passes no x) — into a float32
+    accumulator (numpy_groupies check_dtype keeps the input dtype; numba forms
+    f32(a_i + a_{i+1}) / 2 in float64 and rounds the sum to float32 on every +=).
+    Sequential in point order.  Bins with < 2 points stay 0 (fill_value)."""
+    rows = np.asarray(rows_f32, dtype=np.float32).reshape(-1, rows_f32.shape[-1])
+    n = end - start
+    acc = np.zeros((rows.shape[0], start.size), dtype=np.float32)
+    for j in range(int(n.max()) - 1 if n.size else 0):
+        m = j + 1 < n
+        i = start[m] + j
+        pair = rows[:, i] + rows[:, i + 1]                       # float32 add
+        acc[:, m] = (acc[:, m].astype(np.float64) + pair.astype(np.float64) / 2
+                     ).astype(np.float32)
+    out = acc.astype(np.float64) * (np.asarray(wl_bins)[1:] - np.asarray(wl_bins)[:-1]) * 1e-3
+    return out.reshape(rows_f32.shape[:-1] + (start.size,))
+
+
+def bin_exact_groups(wl_hi, start, end):
+    """Non-empty groups of xarray groupby_bins (empty bins dropped, opacity.py:156) and
+    their coordinates wl.mean() (opacity.py:42)."""
+    keep = end > start
+    gs, ge = start[keep], end[keep]
+    centres = np.array([np.mean(wl_hi[s:e]) for s, e in zip(gs, ge)])
+    return gs, ge, centres
+
+
+def bin_exact_rows(rows_f32, wl_hi, start, end, lam_um):
+    """mapfunc_exact + interp onto lam (opacity.py:33-42, 155-167): per non-empty bin,
+    integrate('wavelength') (xarray trapz: dx * 0.5 * (y[1:] + y[:-1]), float32 pair sum,
+    float64 integrand, summed in point order) / (wl.max() - wl.min()) — a single-point
+    bin gives 0/0 = NaN — at coordinate wl.mean(); then scipy interp1d linear with
+    fill_value='extrapolate' onto lam: slope = (y_hi - y_lo) / (x_hi - x_lo),
+    y = slope * (x - x_lo) + y_lo, interval = clip(searchsorted(x, lam), 1, n - 1)."""
+    rows = np.asarray(rows_f32, dtype=np.float32).reshape(-1, rows_f32.shape[-1])
+    wl_hi = np.asarray(wl_hi, dtype=float)
+    gs, ge, x = bin_exact_groups(wl_hi, start, end)
+    if x.size < 2:
+        raise ValueError("x and y arrays must have at least 2 entries")
+    y = np.zeros((rows.shape[0], x.size))
+    n = ge - gs
+    with np.errstate(invalid="ignore", divide="ignore"):
+        for j in range(int(n.max()) - 1):        # point order within every group
+            m = j + 1 < n
+            i = gs[m] + j
+            integrand = (wl_hi[i + 1] - wl_hi[i]) * 0.5 * (rows[:, i + 1] + rows[:, i])
+            y[:, m] = y[:, m] + integrand
+        y = y / (wl_hi[ge - 1] - wl_hi[gs])
+        lam = np.asarray(lam_um, dtype=float)
+        hi = np.clip(np.searchsorted(x, lam), 1, x.size - 1)
+        lo = hi - 1
+        slope = (y[:, hi] - y[:, lo]) / (x[hi] - x[lo])
+        out = slope * (lam - x[lo]) + y[:, lo]
+    return out.reshape(rows_f32.shape[:-1] + (lam.size,))
+
+
+def binned_opacity(xsec, xsec_T, xsec_p, wl_hi, temperatures, pressures_bar, wl_bins, lam_um,
+                   groupies=True):
+    """One species of binned_opacity (opacity.py:66-170) -> (pressure, temperature, λ)
+    table (this oracle's Table layout; the reference's DataArray is (temperature,
+    pressure, wavelength) for groupies and (wavelength, temperature, pressure) for the
+    exact path)."""
+    start, end = bin_ranges(wl_hi, wl_bins)
+    ti = nearest_index(xsec_T, temperatures)
+    pi = nearest_index(xsec_p, pressures_bar)
+    # bin only the source rows the nearest selection uses (selection commutes with binning)
+    pairs = sorted({(a, b) for a in ti for b in pi})
+    rows = np.stack([xsec[a, b] for a, b in pairs])
+    binned = (bin_groupies_rows(rows, start, end, wl_bins) if groupies
+              else bin_exact_rows(rows, wl_hi, start, end, lam_um))
+    where = {pq: k for k, pq in enumerate(pairs)}
+    out = np.empty((len(pi), len(ti), binned.shape[-1]))
+    for kp, b in enumerate(pi):
+        for kt, a in enumerate(ti):
+            out[kp, kt] = binned[where[(a, b)]]
+    return out

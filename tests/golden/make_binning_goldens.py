@@ -1,0 +1,104 @@
+"""Golden vectors of the reference's opacity binning (build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 /opt/conda/bin/python3.9 -W ignore tests/golden/make_binning_goldens.py
+
+Runs the reference's own ``frei.opacity.binned_opacity`` (opacity.py:66-170) in both
+branches — ``groupies=True`` (interp.py:270-307 ``groupby_bins_agg`` with the numba
+``AggregateTrapz`` loop, interp.py:156-207) and ``groupies=False`` (``mapfunc_exact``,
+opacity.py:33-42, the ``Grid.load_opacities`` default) — on a synthetic high-resolution
+cross-section in the ``opacity_dir_to_netcdf`` layout (opacity.py:395-483: float32
+(temperature, pressure, wavelength), wavelength = 1e4 / wavenumber reversed to
+ascending).  Stand-ins: ``binharness`` (numba identity jit, numpy_groupies and xarray
+restatements; pandas is real).  Writes ``binning.npz`` (inputs + outputs, no pickles).
+"""
+import os
+import shutil
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import binharness as BH  # noqa: E402
+
+import numpy as np  # noqa: E402
+import astropy.units as u  # noqa: E402
+
+R = BH.load()
+
+
+def xsec_grid():
+    """Synthetic DACE-like grid: 5 T x 4 p nodes, 15,200 wavenumber points."""
+    wlen = np.arange(1000, 20000, 1.25)                      # cm^-1 (opacity.py:409)
+    wavelength = 1 / wlen / 1e-4                             # µm (opacity.py:412)
+    wl = wavelength[1:][::-1]                                # ascending (opacity.py:414)
+    tgrid = np.array([600.0, 1200.0, 1800.0, 2400.0, 3000.0])
+    pgrid = 10.0 ** np.array([-6.0, -3.0, 0.0, 2.0])
+    rng = np.random.default_rng(7)
+    x = np.log(wl)
+    logk = -1.5 + 0.9 * np.sin(1.7 * x) + 0.4 * np.cos(6.1 * x)
+    centres = rng.uniform(x.min(), x.max(), 400)
+    depth = rng.lognormal(0.0, 1.0, 400)
+    width = rng.uniform(2e-4, 2e-3, 400)
+    prof = np.zeros_like(x)
+    for c, d, w in zip(centres, depth, width):
+        m = np.abs(x - c) < 8 * w
+        prof[m] += d / (1 + ((x[m] - c) / w) ** 2)
+    base = 10 ** (logk + prof)
+    op = (base[None, None, :] * (tgrid[:, None, None] / 1000.0) ** 0.5
+          * pgrid[None, :, None] ** 0.05).astype(np.float32)
+    op[1, 2, ::97] = 0.0          # a few exact zeros
+    return op, tgrid, pgrid, wl
+
+
+def run(path, temperatures, pressures, wl_bins, lam, groupies):
+    res = R.opacity.binned_opacity(temperatures, pressures, wl_bins, lam,
+                                   groupies=groupies, path=path)
+    (iso, arr), = res.items()
+    return iso, arr
+
+
+def main():
+    op, tgrid, pgrid, wl = xsec_grid()
+    tmp = tempfile.mkdtemp(prefix="frei_bin_")
+    try:
+        BH.register(tmp, "1H2-16O", op, tgrid, pgrid, wl)
+        path = os.path.join(tmp, "*.nc")
+        out = dict(xsec=op, xsec_T=tgrid, xsec_p=pgrid, xsec_wl=wl)
+        pl = R.core.Planet.from_hot_jupiter()
+        cases = {
+            "g1": R.core.Grid(pl, n_layers=6, T_ref=2400 * u.K),
+            "g2": R.core.Grid(pl, n_layers=4, n_wl_bins=6000, T_ref=2400 * u.K),
+        }
+        for name, g in cases.items():
+            T, p = g.init_temperatures, g.pressures
+            out[f"{name}_T"] = T.to(u.K).value
+            out[f"{name}_p"] = p.to(u.bar).value
+            out[f"{name}_lam"] = g.lam.to(u.um).value
+            out[f"{name}_wl_bins"] = np.asarray(g.wl_bins)
+            iso, a = run(path, T, p, g.wl_bins, g.lam, True)
+            assert a.dims == ("temperature", "pressure", "wavelength"), a.dims
+            out[f"{name}_groupies"] = a.values
+            iso, b = run(path, T, p, g.wl_bins, g.lam, False)
+            assert b.dims == ("wavelength", "temperature", "pressure"), b.dims
+            out[f"{name}_exact"] = b.values
+            out[f"{name}_exact_wl"] = b.coords["wavelength"]
+            print(name, iso, a.values.shape, b.values.shape,
+                  "nan(exact):", int(np.isnan(b.values).sum()))
+        # nearest-node ties (midpoints -> lower node) and extrapolation beyond the nodes
+        g = cases["g1"]
+        T_tie = np.array([100.0, 600.0, 900.0, 1500.0, 2999.0, 5000.0, 1200.0])
+        p_tie = np.array([1e-8, pgrid[1] / 2 + pgrid[2] / 2, 0.3, 50.0, 1e3])
+        out["tie_T"], out["tie_p"] = T_tie, p_tie
+        iso, a = run(path, T_tie * u.K, p_tie * u.bar, g.wl_bins, g.lam, True)
+        out["tie_groupies"] = a.values
+        iso, b = run(path, T_tie * u.K, p_tie * u.bar, g.wl_bins, g.lam, False)
+        out["tie_exact"] = b.values
+        dest = os.path.join(HERE, "binning.npz")
+        np.savez_compressed(dest, **out)
+        print(f"wrote binning.npz: {os.path.getsize(dest) / 1024:.1f} KiB")
+    finally:
+        shutil.rmtree(tmp)
+
+
+if __name__ == "__main__":
+    main()

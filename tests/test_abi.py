@@ -59,3 +59,19 @@ def test_kernel_objects_target_gfx950():
     so = os.path.join(ROOT, "frei_amd", "libfrei_hip.so")
     data = open(so, "rb").read()
     assert b"gfx950" in data
+
+
+def test_binning_argument_errors_without_gpu():
+    """frei_xsec_create validates the high-resolution axis before touching a device."""
+    import ctypes
+    import numpy as np
+    from frei_amd import _native as N
+    lib = N.lib()
+    h = ctypes.c_void_p()
+    vals = np.zeros((1, 1, 4), dtype=np.float32)
+    T, p = np.array([1000.0]), np.array([1.0])
+    wl = np.array([1.0, 2.0, 2.0, 3.0])
+    assert lib.frei_xsec_create(ctypes.byref(h), 0, N.fptr(vals), 1, 1, 4, N.dptr(T), N.dptr(p),
+                                N.dptr(wl)) != 0
+    assert b"ascending" in lib.frei_last_error()
+    assert lib.frei_xsec_bin(None, 0, None, None, 0, None, 0, None, 0, None) != 0

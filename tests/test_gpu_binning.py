@@ -1,0 +1,151 @@
+"""GPU parity of K6, opacity binning (frei/opacity.py:66-170, frei/interp.py:156-307),
+through the C ABI, against the reference's own binned_opacity (tests/golden/binning.npz)
+and the CPU oracle.
+
+groupies mode (float32 accumulator, sequential pair order): bit-exact.
+exact mode (float64 trapezoid integral, then linear interpolation): the NaN pattern of
+single-point bins is identical, values agree to 1e-13 relative (the reference's
+np.sum may sum a bin pairwise, the kernel sums in point order; all terms are >= 0)."""
+import numpy as np
+import pytest
+
+from oracle import frei_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+EXACT_RTOL = 1e-13
+
+
+@pytest.fixture(scope="module")
+def fa():
+    import frei_amd
+    from frei_amd import _native as N
+    assert N.device_count() >= 1, "no HIP device visible"
+    return frei_amd
+
+
+@pytest.fixture(scope="module")
+def xs(fa, golden):
+    B = golden("binning.npz")
+    x = fa.CrossSection(B["xsec"], B["xsec_T"], B["xsec_p"], B["xsec_wl"], "1H2-16O")
+    yield B, x
+    x.release()
+
+
+def _assert_exact(out, ref, what):
+    assert np.array_equal(np.isnan(out), np.isnan(ref)), what + ": NaN pattern"
+    ok = ~np.isnan(ref)
+    err = np.abs(out[ok] - ref[ok])
+    assert np.all(err <= EXACT_RTOL * np.abs(ref[ok])), \
+        f"{what}: max rel {np.max(err / np.abs(ref[ok])):.3e}"
+
+
+@pytest.mark.parametrize("case", ["g1", "g2", "tie"])
+def test_groupies_binning_bit_exact_vs_reference(xs, case):
+    B, x = xs
+    grid = "g1" if case == "tie" else case
+    out = x.bin(B[f"{grid}_wl_bins"], B[f"{grid}_lam"], B[f"{case}_T"], B[f"{case}_p"],
+                groupies=True)
+    ref = np.transpose(B[f"{case}_groupies"], (1, 0, 2))
+    assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("case", ["g1", "g2", "tie"])
+def test_exact_binning_matches_reference(xs, case):
+    B, x = xs
+    grid = "g1" if case == "tie" else case
+    out = x.bin(B[f"{grid}_wl_bins"], B[f"{grid}_lam"], B[f"{case}_T"], B[f"{case}_p"],
+                groupies=False)
+    _assert_exact(out, np.transpose(B[f"{case}_exact"], (2, 1, 0)), case)
+    orc = O.binned_opacity(B["xsec"], B["xsec_T"], B["xsec_p"], B["xsec_wl"], B[f"{case}_T"],
+                           B[f"{case}_p"], B[f"{grid}_wl_bins"], B[f"{grid}_lam"],
+                           groupies=False)
+    assert np.array_equal(np.isnan(out), np.isnan(orc))
+    ok = ~np.isnan(orc)
+    assert np.array_equal(out[ok], orc[ok]), "kernel vs oracle (same summation order)"
+
+
+def test_random_cross_section_large_grid_matches_oracle(fa):
+    """Denser data than the goldens: 3 x 2 source nodes x 300k points onto 50k bins (both
+    modes), target nodes with repeated nearest selections (fan-out of one source row to
+    several table rows)."""
+    rng = np.random.default_rng(11)
+    nu = np.linspace(1000.0, 20000.0, 300_001)
+    wl = (1e4 / nu)[1:][::-1]
+    T_src, p_src = np.array([800.0, 1600.0, 2400.0]), np.array([1e-3, 1.0])
+    xsec = (10 ** rng.uniform(-4, 2, (3, 2, wl.size))).astype(np.float32)
+    lam, wl_bins, _ = O.wavelength_grid(0.5, 10, 50_000)
+    T_t = np.array([700.0, 900.0, 1500.0, 2600.0, 3000.0])
+    p_t = np.array([1e-4, 1e-2, 0.8, 5.0])
+    x = fa.CrossSection(xsec, T_src, p_src, wl)
+    try:
+        for groupies in (True, False):
+            out = x.bin(wl_bins, lam, T_t, p_t, groupies=groupies)
+            ref = O.binned_opacity(xsec, T_src, p_src, wl, T_t, p_t, wl_bins, lam, groupies)
+            assert np.array_equal(np.isnan(out), np.isnan(ref))
+            ok = ~np.isnan(ref)
+            assert np.array_equal(out[ok], ref[ok]), f"groupies={groupies}"
+    finally:
+        x.release()
+
+
+def test_grid_bins_into_device_tables_and_runs(fa, golden):
+    """Grid.load_opacities(cross_sections=...) bins on the device straight into the engine
+    tables; the T-P loop result equals the same run on the host-binned tables uploaded
+    with frei_set_table (bitwise), and matches the oracle on the oracle-binned tables."""
+    B = golden("binning.npz")
+    planet = fa.Planet.from_hot_jupiter()
+    for groupies in (True, False):
+        grid = fa.Grid(planet, n_layers=6, T_ref=2400)
+        x = fa.CrossSection(B["xsec"], B["xsec_T"], B["xsec_p"], B["xsec_wl"], "1H2-16O")
+        grid.load_opacities(cross_sections={"1H2-16O": x}, groupies=groupies)
+        spec, T, th, dt = grid.emission_spectrum(n_timesteps=3)
+        tab = grid.opacities["1H2-16O"]
+        host = fa.OpacityTable(tab.values, tab.pressure, tab.temperature)
+        # this Grid's own arrays (its logspace grid differs from the golden's by ulps)
+        ref_tab = O.binned_opacity(B["xsec"], B["xsec_T"], B["xsec_p"], B["xsec_wl"],
+                                   grid.init_temperatures, grid.pressures, grid.wl_bins,
+                                   grid.lam, groupies=groupies)
+        assert np.array_equal(np.isnan(host.values), np.isnan(ref_tab))
+        ok = ~np.isnan(ref_tab)
+        assert np.array_equal(host.values[ok], ref_tab[ok])
+        grid2 = fa.Grid(planet, n_layers=6, T_ref=2400)
+        grid2.load_opacities(opacities={"1H2-16O": host})
+        spec2, T2, th2, dt2 = grid2.emission_spectrum(n_timesteps=3)
+        assert np.array_equal(T, T2) and np.array_equal(spec.flux, spec2.flux)
+        assert np.array_equal(dt, dt2, equal_nan=True)
+        grid._close_engine()
+        grid2._close_engine()
+        x.release()
+
+
+def test_sharded_binning_matches_whole_grid(fa, golden):
+    """A context owning a wavelength slice bins only its slice (exact mode reaches the
+    neighbouring groups outside the slice for the interpolation)."""
+    B = golden("binning.npz")
+    x = fa.CrossSection(B["xsec"], B["xsec_T"], B["xsec_p"], B["xsec_wl"])
+    lam, wl_bins = B["g2_lam"], B["g2_wl_bins"]
+    T_t, p_t = B["g2_T"], B["g2_p"]
+    try:
+        for groupies in (True, False):
+            whole = x.bin(wl_bins, lam, T_t, p_t, groupies=groupies)
+            tab = fa.BinnedTable(x, wl_bins, lam, T_t, p_t, groupies)
+            for lo, hi in [(0, 1000), (1000, 3001), (3001, 6000)]:
+                eng = fa.Engine(lam, p_t, {"s": tab},
+                                lam_slice=(lo, hi))
+                try:
+                    k, _ = eng.kappa(float(T_t[1]), float(p_t[1]))
+                finally:
+                    eng.close()
+                # kappa at an on-node (T, p): mmr * table row + sigma, table row = whole[1, 1]
+                eng_w = fa.Engine(lam, p_t, {"s": fa.OpacityTable(whole, p_t, T_t)},
+                                  lam_slice=(lo, hi))
+                try:
+                    kw, _ = eng_w.kappa(float(T_t[1]), float(p_t[1]))
+                finally:
+                    eng_w.close()
+                assert np.array_equal(np.isnan(k), np.isnan(kw))
+                ok = ~np.isnan(kw)
+                assert np.array_equal(k[ok], kw[ok]), (groupies, lo, hi)
+    finally:
+        x.release()
