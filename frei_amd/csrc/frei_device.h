@@ -249,6 +249,8 @@ void launch_gen_table(double* tab, const double* base, const double* fp, const d
                       int n_p, int n_T, int64_t n_lam, int64_t stride, double lo, double hi,
                       hipStream_t st);
 void launch_fill(double* x, int64_t n, double v, hipStream_t st);
+void launch_contract(const double* const* tabs, int S, const double* mmr, const int32_t* prow,
+                     int n_layers, int n_T, int64_t pitch, double* eff, hipStream_t st);
 
 // Error reporting shared by the runtime and the binning module (frei_last_error()).
 int set_error(const std::string& msg);

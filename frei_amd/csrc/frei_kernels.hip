@@ -778,6 +778,44 @@ __global__ void gen_table_kernel(double* tab, const double* base, const double* 
   }
 }
 
+// Species contraction of the shared-bracket tables: for every layer l
+// and T node t, eff[prow_l][t][:] = sum_s mmr[s][l] * tab_s[prow_l][t][:] in species
+// order (no FMA).  The sweep then interpolates this one table (mmr = 1), reading 2 rows
+// per layer instead of 2 S.
+struct ContractArgs {
+  const double* tab[kMaxFastS];
+  const double* mmr;      // [S][n_layers]
+  const int32_t* prow;    // [n_layers] table pressure row of each layer
+  double* eff;
+  int S, n_layers, n_T;
+  int64_t pitch;
+};
+
+__global__ __launch_bounds__(256) void contract_kernel(ContractArgs a) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.pitch) return;
+  const int l = blockIdx.y, t = blockIdx.z;
+  const int64_t idx = ((int64_t)a.prow[l] * a.n_T + t) * a.pitch + j;
+  double acc = a.mmr[l] * a.tab[0][idx];
+  for (int s = 1; s < a.S; ++s) acc = acc + a.mmr[(int64_t)s * a.n_layers + l] * a.tab[s][idx];
+  a.eff[idx] = acc;
+}
+
+void launch_contract(const double* const* tabs, int S, const double* mmr, const int32_t* prow,
+                     int n_layers, int n_T, int64_t pitch, double* eff, hipStream_t st) {
+  ContractArgs a{};
+  for (int s = 0; s < S && s < kMaxFastS; ++s) a.tab[s] = tabs[s];
+  a.mmr = mmr;
+  a.prow = prow;
+  a.eff = eff;
+  a.S = S;
+  a.n_layers = n_layers;
+  a.n_T = n_T;
+  a.pitch = pitch;
+  dim3 grid((unsigned)((pitch + 255) / 256), (unsigned)n_layers, (unsigned)n_T);
+  hipLaunchKernelGGL(contract_kernel, grid, dim3(256), 0, st, a);
+}
+
 __global__ void fill_kernel(double* x, int64_t n, double v) {
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
        idx += (int64_t)gridDim.x * blockDim.x)

@@ -126,6 +126,15 @@ struct frei_ctx {
   FastStep* d_fsteps = nullptr;
   FastStepS* d_ssteps = nullptr;
   int shared = 0;   // fast path with one bracket for all species (identical nodes)
+  // Species-contracted table (K3): with shared nodes, no NaN and fixed per-layer mmr the
+  // sweep reads eff[p][t][:] = sum_s mmr_s(l) tab_s[p][t][:] (2 rows per layer, not 2 S).
+  // FREI_PRECONTRACT=0 keeps the per-species sum inside the sweep.
+  int eff = 0, eff_mode = -1;
+  double* d_eff = nullptr;
+  size_t eff_cap = 0;
+  SpecMeta* d_smeta_eff = nullptr;
+  double* d_ones = nullptr;
+  int32_t* d_prow = nullptr;
   double *d_part = nullptr, *d_Fb = nullptr, *d_Fb_all = nullptr;
   // T-P loop state
   int* d_conv = nullptr;
@@ -177,6 +186,55 @@ void dfree(T*& p) {
 template <typename T>
 int h2d(T* d, const T* h, size_t n, hipStream_t st) {
   HIP_TRY(hipMemcpyAsync(d, h, n * sizeof(T), hipMemcpyHostToDevice, st));
+  return 0;
+}
+
+// Species contraction (K3) when every species shares its nodes (one bracket per layer), no
+// table holds a NaN (the reference's nansum, Q8, is per species) and S >= 2.
+int build_contracted(frei_ctx* c, bool shared_fast) {
+  const int nL = c->nL, S = c->S;
+  bool on = shared_fast && S >= 2 && c->eff_mode != 0;
+  for (int s = 0; s < S && on; ++s) on = !c->sp[s].has_nan;
+  std::vector<int32_t> prow(nL, 0);
+  if (on) {
+    std::vector<int> owner((size_t)c->sp[0].n_p, -1);
+    for (int l = 0; l < nL && on; ++l) {
+      const PMeta& pm = c->pmeta[l];  // species 0 (shared nodes)
+      prow[l] = (pm.wp_lo != 0.0) ? pm.p_lo : pm.p_hi;
+      if (owner[prow[l]] >= 0) {  // two layers on one pressure row: mmr must agree
+        for (int s = 0; s < S && on; ++s)
+          on = c->mmr[(size_t)s * nL + l] == c->mmr[(size_t)s * nL + owner[prow[l]]];
+      }
+      owner[prow[l]] = l;
+    }
+  }
+  c->eff = on ? 1 : 0;
+  if (!on) return 0;
+  const Species& q0 = c->sp[0];
+  const size_t need = (size_t)q0.n_p * q0.n_T * (size_t)q0.stride + 64;
+  if (c->eff_cap < need) {
+    dfree(c->d_eff);
+    c->eff_cap = 0;
+    TRY(dalloc(&c->d_eff, need));
+    c->eff_cap = need;
+  }
+  HIP_TRY(hipMemsetAsync(c->d_eff, 0, need * sizeof(double), c->stream));
+  if (!c->d_ones) {
+    std::vector<double> ones(nL, 1.0);
+    TRY(dalloc(&c->d_ones, nL));
+    TRY(h2d(c->d_ones, ones.data(), nL, c->stream));
+  }
+  dfree(c->d_prow);
+  TRY(dalloc(&c->d_prow, nL));
+  TRY(h2d(c->d_prow, prow.data(), nL, c->stream));
+  const double* tabs[kMaxFastS];
+  for (int s = 0; s < S; ++s) tabs[s] = c->sp[s].d_tab;
+  launch_contract(tabs, S, c->d_mmr, c->d_prow, nL, q0.n_T, q0.stride, c->d_eff, c->stream);
+  HIP_TRY(hipGetLastError());
+  SpecMeta m = c->smeta[0];
+  m.tab = c->d_eff;
+  if (!c->d_smeta_eff) TRY(dalloc(&c->d_smeta_eff, 1));
+  TRY(h2d(c->d_smeta_eff, &m, 1, c->stream));
   return 0;
 }
 
@@ -274,6 +332,7 @@ int build_meta(frei_ctx* c) {
   TRY(h2d(c->d_tperm, c->tperm.data(), c->tperm.size(), c->stream));
   if (c->mmr.size() != (size_t)S * nL) return fail("frei_set_mmr must be called");
   TRY(h2d(c->d_mmr, c->mmr.data(), (size_t)S * nL, c->stream));
+  TRY(build_contracted(c, fast && shared));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->meta_dirty = false;
   return 0;
@@ -282,18 +341,18 @@ int build_meta(frei_ctx* c) {
 SetupArgs setup_args(frei_ctx* c) {
   SetupArgs u{};
   u.n_layers = c->nL;
-  u.n_species = c->S;
+  u.n_species = c->eff ? 1 : c->S;
   u.fast = c->fast;
   u.T = c->d_T;
   u.p = c->d_p;
   u.p_top2 = c->p_top2;
   u.g = c->g;
-  u.spec = c->d_smeta;
+  u.spec = c->eff ? c->d_smeta_eff : c->d_smeta;
   u.pmeta = c->d_pmeta;
   u.tnodes = c->d_tnodes;
   u.n_tnodes = (int)c->tnodes.size();
   u.tperm = c->d_tperm;
-  u.mmr = c->d_mmr;
+  u.mmr = c->eff ? c->d_ones : c->d_mmr;
   u.steps = c->d_steps;
   u.terms = c->d_terms;
   u.fsteps = c->d_fsteps;
@@ -366,7 +425,9 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     f.sig = c->d_sig;
     f.wtr = c->d_wtr;
     f.ftoa = c->d_ftoa;
+    const int S_run = c->eff ? 1 : c->S;
     for (int q = 0; q < kMaxFastS; ++q) f.tab[q] = q < c->S ? c->sp[q].d_tab : nullptr;
+    if (c->eff) f.tab[0] = c->d_eff;
     f.steps = c->d_fsteps;
     f.ssteps = c->d_ssteps;
     f.F_up = c->d_Fu;
@@ -379,8 +440,8 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     const int depth = c->prefetch_depth > 0 ? c->prefetch_depth : 2;
     bool nan_check = false;
     for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
-    launch_sweep_fast(o.dir, c->S, depth, nan_check, c->shared != 0, f, c->nblocks,
-                      c->stream);
+    launch_sweep_fast(o.dir, S_run, depth, nan_check && !c->eff, c->shared != 0, f,
+                      c->nblocks, c->stream);
   } else {
     launch_sweep(o.dir, a, c->nblocks, false, c->stream);
   }
@@ -434,8 +495,9 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   u.iter = c->d_iter;
   u.conv = c->d_conv;
   // metadata in LDS when the whole update stays within 64 KiB of LDS
-  u.meta_in_lds = ((size_t)c->S * c->nL * (sizeof(PMeta) + sizeof(double)) +
-                   (size_t)c->S * sizeof(SpecMeta) + (size_t)12 * c->nL * sizeof(double) +
+  const size_t S_meta = c->eff ? 1 : c->S;
+  u.meta_in_lds = (S_meta * c->nL * (sizeof(PMeta) + sizeof(double)) +
+                   S_meta * sizeof(SpecMeta) + (size_t)12 * c->nL * sizeof(double) +
                    c->tnodes.size() * sizeof(double)) <= 64 * 1024;
   launch_update(u, c->stream);
   HIP_TRY(hipGetLastError());
@@ -500,6 +562,7 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
   if (const char* e = getenv("FREI_PREFETCH_DEPTH")) c->prefetch_depth = atoi(e);
   if (const char* e = getenv("FREI_SHARED")) c->shared_mode = atoi(e) ? 1 : 0;
   if (const char* e = getenv("FREI_SHARED_MAX_BLOCKS")) c->shared_max_blocks = atoi(e);
+  if (const char* e = getenv("FREI_PRECONTRACT")) c->eff_mode = atoi(e) ? 1 : 0;
   auto bail = [&](int rc) {
     frei_ctx_destroy(c);
     return rc;
@@ -547,6 +610,10 @@ int frei_ctx_destroy(frei_ctx* c) {
     if (r && r->commDestroy) r->commDestroy(c->comm);
   }
   for (auto& s : c->sp) dfree(s.d_tab);
+  dfree(c->d_eff);
+  dfree(c->d_smeta_eff);
+  dfree(c->d_ones);
+  dfree(c->d_prow);
   double* dd[] = {c->d_c1, c->d_lk, c->d_sig, c->d_ftoa, c->d_wtr, c->d_p, c->d_lnp,
                   c->d_Fu, c->d_Fd, c->d_T, c->d_dT, c->d_dtaus, c->d_bol, c->d_tnodes, c->d_mmr, c->d_part,
                   c->d_Fb, c->d_Fb_all, c->d_Tb, c->d_Ta, c->d_hist};

@@ -131,14 +131,14 @@ def test_sharded_binning_matches_whole_grid(fa, golden):
             whole = x.bin(wl_bins, lam, T_t, p_t, groupies=groupies)
             tab = fa.BinnedTable(x, wl_bins, lam, T_t, p_t, groupies)
             for lo, hi in [(0, 1000), (1000, 3001), (3001, 6000)]:
-                eng = fa.Engine(lam, p_t, {"s": tab},
+                eng = fa.Engine(lam, p_t, {"1H2-16O": tab},
                                 lam_slice=(lo, hi))
                 try:
                     k, _ = eng.kappa(float(T_t[1]), float(p_t[1]))
                 finally:
                     eng.close()
                 # kappa at an on-node (T, p): mmr * table row + sigma, table row = whole[1, 1]
-                eng_w = fa.Engine(lam, p_t, {"s": fa.OpacityTable(whole, p_t, T_t)},
+                eng_w = fa.Engine(lam, p_t, {"1H2-16O": fa.OpacityTable(whole, p_t, T_t)},
                                   lam_slice=(lo, hi))
                 try:
                     kw, _ = eng_w.kappa(float(T_t[1]), float(p_t[1]))
