@@ -11,7 +11,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # FREI_HIP_LIB overrides the library path (A/B builds of the same ABI, tools/ab_sweep.py)
-LIB_PATH = os.environ.get("FREI_HIP_LIB") or os.path.join(_HERE, "libfrei_hip.so")
+_DEFAULT_LIB = os.path.join(_HERE, "libfrei_hip.so")
+LIB_PATH = os.environ.get("FREI_HIP_LIB") or _DEFAULT_LIB
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -57,6 +58,7 @@ SIGNATURES = {
     "frei_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp]),
     "frei_comm_init_host": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
                                            "ALLGATHER_FN", _vp]),
+    "frei_ctx_path": (ctypes.c_int, [_vp, _ip]),
     "frei_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "frei_timing_read": (ctypes.c_int, [_vp, _dp, _ip]),
     "frei_xsec_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, _fp, ctypes.c_int,
@@ -85,6 +87,8 @@ def lib():
                                "`python -m frei_amd.build` (no CPU fallback exists)")
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
         for name, (res, args) in SIGNATURES.items():
+            if LIB_PATH != _DEFAULT_LIB and not hasattr(L, name):
+                continue  # an older A/B build (FREI_HIP_LIB) may predate an entry point
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = [ALLGATHER_FN if a == "ALLGATHER_FN" else a for a in args]

@@ -35,10 +35,25 @@ __device__ __forceinline__ double planck(double c1, double lk, double T) {
 __device__ __forceinline__ void two_stream(double w0, double dtau, double B1, double B2,
                                            double F1u, double F2d, double& F2u,
                                            double& F1d) {
-  const double E = (w0 > 0.1) ? ((1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0)) : 1.0;
-  const double Emw = E - w0;
-  const double Tr = exp((-2.0 * sqrt(E * Emw)) * dtau);
-  const double r = sqrt(Emw / E);
+  // E = 1 where w0 <= 0.1 (twostream.py:90-94): then E * Emw, Emw / E and Bprime / (2 E)
+  // are exact without the multiply/divide, and sqrt(E * Emw) == sqrt(Emw / E), so that
+  // branch skips two divisions and a square root with bit-identical results.
+  double E, Emw, sq, r, q;
+  const double Bp = (B1 - B2) / dtau;
+  if (w0 > 0.1) {
+    E = (1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0);
+    Emw = E - w0;
+    sq = sqrt(E * Emw);
+    r = sqrt(Emw / E);
+    q = Bp / (2.0 * E);
+  } else {
+    E = 1.0;
+    Emw = 1.0 - w0;
+    sq = sqrt(Emw);
+    r = sq;
+    q = Bp * 0.5;
+  }
+  const double Tr = exp((-2.0 * sq) * dtau);
   const double zp = 0.5 * (1.0 + r);
   const double zm = 0.5 * (1.0 - r);
   const double Tr2 = Tr * Tr;
@@ -48,7 +63,6 @@ __device__ __forceinline__ void two_stream(double w0, double dtau, double B1, do
   const double xi = (zp * zm) * (1.0 - Tr2);
   const double psi = (zm2 - zp2) * Tr;
   const double pi_w = (kPi * (1.0 - w0)) / Emw;
-  const double q = ((B1 - B2) / dtau) / (2.0 * E);
   const double ic = 1.0 / chi;
   F2u = ic * ((psi * F1u - xi * F2d) +
               pi_w * ((B2 * (chi + xi) - psi * B1) + q * ((chi - psi) - xi)));
@@ -245,10 +259,25 @@ struct StepCoef {
 __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, double B2,
                                           StepCoef& c) {
   // twostream.py:139-176, same order as two_stream()
-  const double E = (w0 > 0.1) ? ((1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0)) : 1.0;
-  const double Emw = E - w0;
-  const double Tr = exp((-2.0 * sqrt(E * Emw)) * dtau);
-  const double r = sqrt(Emw / E);
+  // E = 1 where w0 <= 0.1 (twostream.py:90-94): then E * Emw, Emw / E and Bprime / (2 E)
+  // are exact without the multiply/divide, and sqrt(E * Emw) == sqrt(Emw / E), so that
+  // branch skips two divisions and a square root with bit-identical results.
+  double E, Emw, sq, r, q;
+  const double Bp = (B1 - B2) / dtau;
+  if (w0 > 0.1) {
+    E = (1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0);
+    Emw = E - w0;
+    sq = sqrt(E * Emw);
+    r = sqrt(Emw / E);
+    q = Bp / (2.0 * E);
+  } else {
+    E = 1.0;
+    Emw = 1.0 - w0;
+    sq = sqrt(Emw);
+    r = sq;
+    q = Bp * 0.5;
+  }
+  const double Tr = exp((-2.0 * sq) * dtau);
   const double zp = 0.5 * (1.0 + r);
   const double zm = 0.5 * (1.0 - r);
   const double Tr2 = Tr * Tr;
@@ -258,7 +287,6 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
   const double xi = (zp * zm) * (1.0 - Tr2);
   const double psi = (zm2 - zp2) * Tr;
   const double pi_w = (kPi * (1.0 - w0)) / Emw;
-  const double q = ((B1 - B2) / dtau) / (2.0 * E);
   c.psi = psi;
   c.xi = xi;
   c.ic = 1.0 / chi;

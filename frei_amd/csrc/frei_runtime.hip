@@ -1093,6 +1093,16 @@ int frei_comm_init_host(frei_ctx* c, int nranks, int rank, frei_allgather_fn fn,
   return 0;
 }
 
+int frei_ctx_path(frei_ctx* c, int* flags) {
+  if (!ready(c) || !flags) return fail("context not ready or null argument");
+  TRY(set_device(c));
+  TRY(build_meta(c));
+  int nan = 0;
+  for (const auto& q : c->sp) nan = nan || q.has_nan;
+  *flags = (c->fast ? 1 : 0) | (c->fast && c->shared ? 2 : 0) | (c->eff ? 4 : 0) | (nan ? 8 : 0);
+  return 0;
+}
+
 int frei_timing_enable(frei_ctx* c, int on) {
   if (!c) return fail("null argument");
   TRY(set_device(c));

@@ -236,6 +236,14 @@ class Engine:
         N.check(N.lib().frei_timing_read(self._ctx, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def path(self):
+        """Sweep implementation the tables select: dict(fast, lds_steps, contracted, nan)."""
+        f = ctypes.c_int(0)
+        N.check(N.lib().frei_ctx_path(self._ctx, ctypes.byref(f)))
+        v = f.value
+        return dict(fast=bool(v & 1), lds_steps=bool(v & 2), contracted=bool(v & 4),
+                    nan=bool(v & 8))
+
     def kappa(self, T, p_bar):
         k = np.empty(self.n_lam)
         sig = np.empty(self.n_lam)

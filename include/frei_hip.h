@@ -146,6 +146,12 @@ int frei_comm_init(frei_ctx* ctx, int nranks, int rank, const void* id128);
 typedef int (*frei_allgather_fn)(const double* send, double* recv, int64_t n, void* user);
 int frei_comm_init_host(frei_ctx* ctx, int nranks, int rank, frei_allgather_fn fn, void* user);
 
+/* Which sweep implementation the context's current tables select (after metadata build):
+ * bit 0 fast path (on-node pressures, >= 2 T nodes, S <= 8), bit 1 step table staged in
+ * LDS (shared brackets, small slices), bit 2 species-contracted table (K3), bit 3 tables
+ * hold NaN (per-species nansum variant). */
+int frei_ctx_path(frei_ctx* ctx, int* flags);
+
 /* Timing of the sweep kernel (HIP events on the context stream around every sweep
  * launch while enabled): total milliseconds and number of timed launches. */
 int frei_timing_enable(frei_ctx* ctx, int on);

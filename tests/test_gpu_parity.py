@@ -283,3 +283,46 @@ def test_generic_sweep_path_matches_oracle(fa, mode):
     assert_flux_parity(up, ou, cond["up"], delta, mode + " F_up")
     assert_flux_parity(down, od, cond["down"], delta, mode + " F_down")
     assert row_normwise(dtaus, odt) < 1e-10
+
+
+def test_species_contraction_matches_per_species_sum(fa, monkeypatch):
+    """K3: the precontracted table (sum_s mmr_s tab_s per node row, then interpolation)
+    against the in-sweep per-species sum (FREI_PRECONTRACT=0) and the oracle, 8 species
+    with layer-dependent mmr, 3 T-P iterations."""
+    rng = np.random.default_rng(5)
+    lam, _, _ = O.wavelength_grid(0.5, 10, 3000)
+    p = O.pressure_grid(40, -6, np.log10(200))
+    T0 = O.temperature_grid(p, 1700.0, 0.1, 0.1)
+    Tn = np.linspace(0.8 * T0.min(), 1.2 * T0.max(), 12)
+    names = ["1H2-16O", "12C-16O", "12C-16O2", "12C-1H4", "Na", "K", "H2-H2", "H2-He"]
+    mmr = np.vstack([O.mock_mmr(names[:6], M_BAR)[:, None] * np.ones(40),
+                     1e-3 * (p / p[0]) ** 0.5, 5e-4 * np.ones(40)])
+    tabs_o, tabs_f = {}, {}
+    for n in names:
+        base = 10 ** rng.uniform(-3, 1, lam.size)
+        fp, fT = (p / 1.0) ** 0.1, (Tn / 1000.0) ** 0.5
+        tabs_o[n] = O.Table(O.separable_table(base, fp, fT), p, Tn)
+        tabs_f[n] = fa.SeparableTable(base, fp, fT, p, Tn)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("FREI_PRECONTRACT", mode)
+        eng = fa.Engine(lam, p, tabs_f, mmr=mmr)
+        try:
+            assert eng.path()["contracted"] == (mode == "1")
+            out[mode] = eng.run(T0, n_timesteps=3, n_zero_crossings=10 ** 6,
+                                convergence_dT=-1.0)
+            out[mode]["fluxes"] = eng.get_fluxes()
+        finally:
+            eng.close()
+    cond = _cond((40, lam.size))
+    osp, oT, oth, odt, ou, od, it = O.emission_spectrum(
+        tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1, n_timesteps=3,
+        n_zero_crossings=10 ** 6, convergence_dT=-1, mmr=mmr, err=cond)
+    for mode in ("1", "0"):
+        relT = rel(out[mode]["final_T"], oT)
+        assert relT < 1e-10
+        delta = max(EPS, relT)
+        assert_flux_parity(out[mode]["spectrum"], osp, cond["up"][-1], delta, "spectrum " + mode)
+        up, down = out[mode]["fluxes"]
+        assert_flux_parity(up, ou, cond["up"], delta, "F_up " + mode)
+        assert_flux_parity(down, od, cond["down"], delta, "F_down " + mode)

@@ -28,6 +28,7 @@ def main():
     n_lam = int(opts.get("n-lam", 500000))
     nL = int(opts.get("n-layers", 60))
     S = int(opts.get("species", 8))
+    contracted = opts.get("contracted", "1") == "1"   # K3: the sweep reads one table
     fetch = per_kernel(f"{fdir}/run_counter_collection.csv", "FETCH_SIZE")
     write = per_kernel(f"{wdir}/run_counter_collection.csv", "WRITE_SIZE")
     kernels = {}
@@ -37,8 +38,10 @@ def main():
         kernels[k] = {"fetch_size_B": fetch[k], "read_B_corrected": rd, "write_B": wr,
                       "hbm_B": rd + wr}
     mean = sum(v["hbm_B"] for v in kernels.values()) / max(len(kernels), 1)
-    alg = (8 + 8 + 16 * S) * (nL - 1) * n_lam   # T-P loop sweep (dead stores removed)
-    json.dump({"workload": {"n_lam": n_lam, "n_layers": nL, "species": S},
+    S_run = 1 if contracted else S
+    alg = (8 + 8 + 16 * S_run) * (nL - 1) * n_lam   # T-P loop sweep (dead stores removed)
+    json.dump({"workload": {"n_lam": n_lam, "n_layers": nL, "species": S,
+                            "contracted": contracted},
                "kernels": kernels, "hbm_B_per_launch": mean,
                "algorithmic_B_per_launch": alg, "traffic_over_algorithmic": mean / alg,
                "correction": "HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halving)"},
