@@ -46,7 +46,9 @@ struct frei_xsec {
 
 namespace {
 
-constexpr int kRB = 8;  // source rows per lane in the exact-mode integration pass
+constexpr int kRB = 4;        // source rows per lane in the exact-mode integration pass
+constexpr int kExpandRows = 8;   // source rows per lane in the exact-mode expand pass
+constexpr int kGroupiesRows = 8;  // source rows per lane in the groupies pass
 
 #define HIP_TRY(expr)                                                                   \
   do {                                                                                  \
@@ -123,6 +125,7 @@ __global__ __launch_bounds__(256) void bin_groupies_kernel(
 // exact, pass 1: xarray integrate (duck_array_ops.trapz) of one non-empty bin for kRB
 // source rows: sum_i (dx_i * 0.5) * f64(f32(y_{i+1} + y_i)) in point order, / (wl_max -
 // wl_min) (opacity.py:40-42; a single-point bin gives 0 / 0 = NaN like the reference).
+// Points are taken four at a time with all loads issued before the ordered adds.
 __global__ __launch_bounds__(256) void bin_exact_integrate_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ row_off, int U,
     const int64_t* __restrict__ gstart, const int64_t* __restrict__ gend,
@@ -142,7 +145,26 @@ __global__ __launch_bounds__(256) void bin_exact_integrate_kernel(
     acc[r] = 0.0;
     prev[r] = rows[r][s];
   }
-  for (int64_t i = s; i + 1 < e; ++i) {
+  int64_t i = s;
+  for (; i + 4 < e; i += 4) {
+    double h[4];
+    float b[kRB][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) h[q] = hdx[i + q];
+#pragma unroll
+    for (int r = 0; r < kRB; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[r][q] = rows[r][i + 1 + q];
+#pragma unroll
+    for (int r = 0; r < kRB; ++r) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[r] = acc[r] + h[q] * (double)(b[r][q] + prev[r]);
+        prev[r] = b[r][q];
+      }
+    }
+  }
+  for (; i + 1 < e; ++i) {
     const double h = hdx[i];
 #pragma unroll
     for (int r = 0; r < kRB; ++r) {
@@ -159,23 +181,25 @@ __global__ __launch_bounds__(256) void bin_exact_integrate_kernel(
 
 // exact, pass 2: scipy interp1d(kind='linear', fill_value='extrapolate') onto the grid
 // wavelengths, slope = (y_hi - y_lo) / (x_hi - x_lo), y = slope * (x - x_lo) + y_lo.
-// One lane per wavelength loops over destination rows [d0, d1) (source row dst_src[d]),
-// so the per-wavelength bracket is read once per lane.
+// One lane per wavelength and source row (rows [u0, u1)): the bracket is read once per
+// lane, each source value pair once, and the result is stored to every destination row
+// that selected this source row (the groupies fan-out).
 __global__ __launch_bounds__(256) void bin_exact_expand_kernel(
-    const double* __restrict__ res, int64_t G, const int32_t* __restrict__ dst_src, int D,
-    int rows_per, const int64_t* __restrict__ dst_off, const int32_t* __restrict__ lo,
-    const double* __restrict__ xlo, const double* __restrict__ xhi,
-    const double* __restrict__ lam, int64_t n, double* __restrict__ out) {
+    const double* __restrict__ res, int64_t G, int U, int rows_per,
+    const int32_t* __restrict__ fan_off, const int64_t* __restrict__ fan_dst,
+    const int32_t* __restrict__ lo, const double* __restrict__ xlo,
+    const double* __restrict__ xhi, const double* __restrict__ lam, int64_t n,
+    double* __restrict__ out) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const int32_t l = lo[j];
   const double dxj = xhi[j] - xlo[j], t = lam[j] - xlo[j];
-  const int d0 = blockIdx.y * rows_per, d1 = min(D, d0 + rows_per);
-  for (int d = d0; d < d1; ++d) {
-    const double* __restrict__ y = res + (int64_t)dst_src[d] * G;
+  const int u0 = blockIdx.y * rows_per, u1 = min(U, u0 + rows_per);
+  for (int u = u0; u < u1; ++u) {
+    const double* __restrict__ y = res + (int64_t)u * G;
     const double ylo = y[l], yhi = y[l + 1];
-    const double slope = (yhi - ylo) / dxj;
-    out[dst_off[d] + j] = slope * t + ylo;
+    const double v = ((yhi - ylo) / dxj) * t + ylo;
+    for (int f = fan_off[u]; f < fan_off[u + 1]; ++f) out[fan_dst[f] + j] = v;
   }
 }
 
@@ -239,15 +263,6 @@ double pairwise_sum(const double* a, int64_t n) {
   return pairwise_sum(a, n2) + pairwise_sum(a + n2, n - n2);
 }
 
-// Rows handled per lane: enough workgroups to fill 256 CUs (~8 per CU) without
-// re-reading the per-wavelength plan once per row.
-int rows_per_lane(int64_t n, int rows) {
-  const int64_t blocks_x = (n + 255) / 256;
-  const int64_t want_y = std::max<int64_t>(1, (2048 + blocks_x - 1) / blocks_x);
-  const int64_t per = (rows + want_y - 1) / want_y;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(per, rows));
-}
-
 struct Dest {
   // destination rows: (p index kp, T index kt) -> element offset in the output
   int n_p = 0, n_T = 0;
@@ -296,6 +311,16 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
     for (int kt = 0; kt < dest.n_T; ++kt)
       dst_src[(size_t)kp * dest.n_T + kt] = uid[(int64_t)ti[kt] * x->np + pi[kp]];
 
+  // fan-out: destination rows of every unique source row (CSR)
+  std::vector<int32_t> fan_off(U + 1, 0);
+  for (int32_t q : dst_src) fan_off[q + 1]++;
+  for (int u = 0; u < U; ++u) fan_off[u + 1] += fan_off[u];
+  std::vector<int64_t> fan_dst(dst_src.size());
+  {
+    std::vector<int32_t> fill(fan_off.begin(), fan_off.end() - 1);
+    for (size_t d = 0; d < dst_src.size(); ++d) fan_dst[fill[dst_src[d]]++] = dest.off[d];
+  }
+
   std::vector<void*> tmp;
   auto cleanup = [&]() {
     (void)hipStreamSynchronize(st);
@@ -314,12 +339,6 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
         e(end.begin() + lam_lo, end.begin() + lam_lo + n_out);
     std::vector<double> w(n_out);
     for (int64_t k = 0; k < n_out; ++k) w[k] = wl_bins[lam_lo + k + 1] - wl_bins[lam_lo + k];
-    std::vector<int32_t> fan_off(U + 1, 0);
-    for (int32_t q : dst_src) fan_off[q + 1]++;
-    for (int u = 0; u < U; ++u) fan_off[u + 1] += fan_off[u];
-    std::vector<int64_t> fan_dst(dst_src.size());
-    std::vector<int32_t> fill(fan_off.begin(), fan_off.end() - 1);
-    for (size_t d = 0; d < dst_src.size(); ++d) fan_dst[fill[dst_src[d]]++] = dest.off[d];
     int64_t *d_s = nullptr, *d_e = nullptr, *d_fd = nullptr;
     double* d_w = nullptr;
     int32_t* d_fo = nullptr;
@@ -329,7 +348,7 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
         (tmp.push_back(d_fo), rc = upload(&d_fd, fan_dst, st)))
       return cleanup(), rc;
     tmp.push_back(d_fd);
-    const int rows_per = rows_per_lane(n_out, U);
+    const int rows_per = std::min(U, kGroupiesRows);
     dim3 grid((unsigned)((n_out + 255) / 256), (unsigned)((U + rows_per - 1) / rows_per));
     if (x->timing) HIP_TRY(hipEventRecord(ev[0], st));
     bin_groupies_kernel<<<grid, 256, 0, st>>>(x->d_x, d_row, U, rows_per, d_s, d_e, d_w, n_out,
@@ -374,7 +393,7 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
     int64_t *d_s = nullptr, *d_e = nullptr, *d_do = nullptr;
     double *d_D = nullptr, *d_res = nullptr, *d_xlo = nullptr, *d_xhi = nullptr,
            *d_lam = nullptr;
-    int32_t *d_lo = nullptr, *d_ds = nullptr;
+    int32_t *d_lo = nullptr, *d_fo = nullptr;
     if ((rc = upload(&d_s, s, st)) || (tmp.push_back(d_s), rc = upload(&d_e, e, st)) ||
         (tmp.push_back(d_e), rc = upload(&d_D, dx, st)) ||
         (tmp.push_back(d_D), rc = dalloc(&d_res, (size_t)U * G)) ||
@@ -382,18 +401,17 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
         (tmp.push_back(d_lo), rc = upload(&d_xlo, xlo, st)) ||
         (tmp.push_back(d_xlo), rc = upload(&d_xhi, xhi, st)) ||
         (tmp.push_back(d_xhi), rc = upload(&d_lam, lamv, st)) ||
-        (tmp.push_back(d_lam), rc = upload(&d_ds, dst_src, st)) ||
-        (tmp.push_back(d_ds), rc = upload(&d_do, dest.off, st)))
+        (tmp.push_back(d_lam), rc = upload(&d_fo, fan_off, st)) ||
+        (tmp.push_back(d_fo), rc = upload(&d_do, fan_dst, st)))
       return cleanup(), rc;
     tmp.push_back(d_do);
     dim3 g1d((unsigned)((G + 255) / 256), (unsigned)((U + kRB - 1) / kRB));
     if (x->timing) HIP_TRY(hipEventRecord(ev[0], st));
     bin_exact_integrate_kernel<<<g1d, 256, 0, st>>>(x->d_x, d_row, U, d_s, d_e, x->d_hdx, d_D,
                                                     G, d_res);
-    const int D = (int)dst_src.size();
-    const int dper = rows_per_lane(n_out, D);
-    dim3 g2d((unsigned)((n_out + 255) / 256), (unsigned)((D + dper - 1) / dper));
-    bin_exact_expand_kernel<<<g2d, 256, 0, st>>>(d_res, G, d_ds, D, dper, d_do, d_lo, d_xlo,
+    const int uper = std::min(U, kExpandRows);
+    dim3 g2d((unsigned)((n_out + 255) / 256), (unsigned)((U + uper - 1) / uper));
+    bin_exact_expand_kernel<<<g2d, 256, 0, st>>>(d_res, G, U, uper, d_fo, d_do, d_lo, d_xlo,
                                                  d_xhi, d_lam, n_out, d_out);
   }
   if (hipGetLastError() != hipSuccess) return cleanup(), set_error("binning kernel launch failed");
