@@ -7,7 +7,8 @@ species-summed opacity assembly, radiative-equilibrium T-P loop): the public nam
 """
 from .binning import BinnedTable, CrossSection, open_cross_section
 from .chemistry import chemistry, iso_to_mass, iso_to_species
-from .core import (B_star, F_TOA, Grid, Planet, Spectrum, effective_temperature,
+from .core import (B_star, F_TOA, Grid, Planet, Spectrum, contribution_function,
+                   effective_temperature,
                    effective_temperature_milne, effective_temperature_planck, wavelength_grid)
 from .engine import Engine, partition, trapz_weights
 from .opacity import (OpacityTable, SeparableTable, binned_opacity, kappa,
@@ -22,4 +23,4 @@ __all__ = ["Planet", "Grid", "Spectrum", "effective_temperature", "wavelength_gr
            "binned_opacity", "rayleigh_H2", "rayleigh_He", "chemistry", "iso_to_species",
            "iso_to_mass", "pressure_grid", "temperature_grid", "propagate_fluxes", "emit",
            "absorb", "BB", "E", "Engine", "partition", "trapz_weights", "CrossSection",
-           "BinnedTable", "open_cross_section"]
+           "BinnedTable", "open_cross_section", "contribution_function"]

@@ -59,6 +59,8 @@ SIGNATURES = {
     "frei_comm_init_host": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
                                            "ALLGATHER_FN", _vp]),
     "frei_ctx_path": (ctypes.c_int, [_vp, _ip]),
+    "frei_milne_pressure": (ctypes.c_int, [_vp, _dp, _dp, _dp]),
+    "frei_contribution": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, ctypes.c_double, _dp]),
     "frei_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "frei_timing_read": (ctypes.c_int, [_vp, _dp, _ip]),
     "frei_xsec_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, _fp, ctypes.c_int,

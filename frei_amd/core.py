@@ -5,14 +5,14 @@
 """
 import numpy as np
 
-from .constants import (A_RSTAR_HOT_JUPITER, G_JUPITER, M_BAR_HOT_JUPITER, SIGMA_SB, UM)
+from .constants import A_RSTAR_HOT_JUPITER, G_JUPITER, M_BAR_HOT_JUPITER, SIGMA_SB, UM
 from .engine import Engine, f_toa
 from .tp import pressure_grid, temperature_grid
 from .twostream import BB
 from .units import scalar, value
 
 __all__ = ["Grid", "Planet", "Spectrum", "effective_temperature", "wavelength_grid", "F_TOA",
-           "B_star"]
+           "B_star", "contribution_function"]
 
 
 def wavelength_grid(min_micron=0.5, max_micron=10, n_bins=500, lam=None):
@@ -95,6 +95,7 @@ class Grid:
         self.mmr = None
         self.device = device
         self._engine = None
+        self._last_dtaus = None
 
     def __repr__(self):
         return (f"<Grid in T=[{self.init_temperatures[0]:.0f}...{self.init_temperatures[-1]:.0f}] K, "
@@ -147,23 +148,46 @@ class Grid:
                                 alpha=self.planet.alpha)
         th = out["temp_hist"]
         th = th.T[th[0] != 0].T   # core.py:320-321
+        self._last_dtaus = out["dtaus"]
         return (Spectrum(out["spectrum"], self.lam), out["final_T"], th, out["dtaus"])
+
+    def contribution_function(self, final_temps, dtaus=None):
+        """Contribution function of the last emission_spectrum (plot.py:63-79)."""
+        return contribution_function(self, self._last_dtaus if dtaus is None else dtaus,
+                                     final_temps)
 
     def emission_dashboard(self, *args, **kwargs):
         raise NotImplementedError("plotting is out of scope for the MI355X engine (SURVEY.md §2)")
 
 
+def _post_engine(grid, dtaus):
+    """The grid's engine and the dtaus argument for the device: None when ``dtaus`` is the
+    array the last emission_spectrum returned (its device copy is used)."""
+    eng = grid.engine()
+    same = dtaus is getattr(grid, "_last_dtaus", None)
+    return eng, (None if same else np.asarray(dtaus, dtype=float))
+
+
 def effective_temperature_milne(grid, spec, dtaus, final_temps):
-    """Photosphere temperature from Milne's tau ~ 2/3 (core.py:386-405)."""
+    """Photosphere temperature from Milne's tau ~ 2/3 (core.py:386-405).  The per-wavelength
+    np.interp over layers runs on the GPU (frei_milne_pressure); the weighted mean and the
+    final interpolation are O(n_lambda) host work, as in the reference."""
     lam = np.asarray(grid.lam)
     p = np.asarray(grid.pressures)
-    pressure_milne = np.ones_like(lam)
-    for i in range(dtaus.shape[1]):
-        pressure_milne[i] = np.interp(2 / 3, np.exp(-dtaus[:, i]), p)
+    eng, d = _post_engine(grid, dtaus)
+    pressure_milne = eng.milne_pressure(p, d)
     # weights: F_lambda -> lambda F_lambda (erg s^-1 cm^-2, astropy spectral_density)
     lam_flux = np.asarray(spec.flux) * (lam * UM)
     return np.interp(np.average(pressure_milne, weights=lam_flux), p[::-1],
                      np.asarray(final_temps)[::-1])
+
+
+def contribution_function(grid, dtaus, final_temps):
+    """Normalised contribution function of the final atmosphere (plot.py:63-79), computed
+    on the GPU: array (n_layers, n_lambda), rows bottom-first like ``grid.pressures`` (the
+    reference plots ``cf[::-1]``)."""
+    eng, d = _post_engine(grid, dtaus)
+    return eng.contribution(np.asarray(grid.pressures), np.asarray(final_temps), d)
 
 
 def effective_temperature_planck(grid, spec):

@@ -249,6 +249,11 @@ void launch_gen_table(double* tab, const double* base, const double* fp, const d
                       int n_p, int n_T, int64_t n_lam, int64_t stride, double lo, double hi,
                       hipStream_t st);
 void launch_fill(double* x, int64_t n, double v, hipStream_t st);
+void launch_milne(const double* dtaus, int nL, int64_t n, const double* fp, double* out,
+                  hipStream_t st);
+void launch_contribution(const double* dtaus, int nL, int64_t n, const double* nu,
+                         const double* ratio, const double* T, double hcperk, double* cf,
+                         hipStream_t st);
 void launch_contract(const double* const* tabs, int S, const double* mmr, const int32_t* prow,
                      int n_layers, int n_T, int64_t pitch, double* eff, hipStream_t st);
 

@@ -844,6 +844,114 @@ void launch_contract(const double* const* tabs, int S, const double* mmr, const 
   hipLaunchKernelGGL(contract_kernel, grid, dim3(256), 0, st, a);
 }
 
+// ---------------------------------------------------------------- post-processing
+// numpy's interp search (npy_interp binary_search_with_guess, LIKELY_IN_CACHE_SIZE 8) for a
+// scalar key over arr(l), l < len: bit-for-bit the index numpy returns, unsorted arrays
+// included (effective_temperature_milne interpolates on unsorted transmissions).
+template <typename Arr>
+__device__ int np_search(double key, int len, int guess, const Arr& arr) {
+  int imin = 0, imax = len;
+  if (key > arr(len - 1)) return len;
+  if (key < arr(0)) return -1;
+  if (len <= 4) {
+    int i = 1;
+    for (; i < len && key >= arr(i); ++i) {
+    }
+    return i - 1;
+  }
+  if (guess > len - 3) guess = len - 3;
+  if (guess < 1) guess = 1;
+  if (key < arr(guess)) {
+    if (key < arr(guess - 1)) {
+      imax = guess - 1;
+      if (guess > 8 && key >= arr(guess - 8)) imin = guess - 8;
+    } else {
+      return guess - 1;
+    }
+  } else {
+    if (key < arr(guess + 1)) return guess;
+    if (key < arr(guess + 2)) return guess + 1;
+    imin = guess + 2;
+    if (guess < len - 8 - 1 && key < arr(guess + 8)) imax = guess + 8;
+  }
+  while (imin < imax) {
+    const int imid = imin + ((imax - imin) >> 1);
+    if (key >= arr(imid)) imin = imid + 1;
+    else imax = imid;
+  }
+  return imin - 1;
+}
+
+// effective_temperature_milne, per wavelength (core.py:392-395):
+// p_milne[j] = np.interp(2/3, exp(-dtaus[:, j]), p_bar) with numpy's search and formula.
+__global__ __launch_bounds__(256) void milne_kernel(const double* __restrict__ dtaus, int nL,
+                                                    int64_t n, const double* __restrict__ fp,
+                                                    double* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  auto X = [&](int l) { return exp(-dtaus[(int64_t)l * n + j]); };
+  const double key = 2.0 / 3.0;
+  const int k = np_search(key, nL, 0, X);
+  double r;
+  if (k == -1) {
+    r = fp[0];
+  } else if (k == nL || k == nL - 1) {
+    r = fp[k == nL ? nL - 1 : k];
+  } else {
+    const double xk = X(k);
+    if (xk == key) {
+      r = fp[k];
+    } else {
+      const double xk1 = X(k + 1);
+      const double slope = (fp[k + 1] - fp[k]) / (xk1 - xk);
+      r = slope * (key - xk) + fp[k];
+      if (isnan(r)) {
+        r = slope * (key - xk1) + fp[k + 1];
+        if (isnan(r) && fp[k] == fp[k + 1]) r = fp[k];
+      }
+    }
+  }
+  out[j] = r;
+}
+
+// Contribution function (plot.py:63-79) per wavelength, layers top-first (the reference's
+// reversed arrays): tau = cumsum of dtau; cf = ((exp(-tau) * dtau) * ratio) * nu^3 /
+// expm1((hc/k * nu) / T), ratio = p / dP; then cf /= sum over layers (sequential, top
+// first).  Written bottom-first (cf[::-1], as plotted).
+__global__ __launch_bounds__(256) void contribution_kernel(
+    const double* __restrict__ dtaus, int nL, int64_t n, const double* __restrict__ nu,
+    const double* __restrict__ ratio, const double* __restrict__ T, double hcperk,
+    double* __restrict__ cf) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const double v = nu[j];
+  const double v3 = pow(v, 3.0);
+  const double hv = hcperk * v;
+  double tau = 0.0, sum = 0.0;
+  for (int m = 0; m < nL; ++m) {
+    const int l = nL - 1 - m;
+    const double d = dtaus[(int64_t)l * n + j];
+    tau = (m == 0) ? d : tau + d;
+    const double c = (((exp(-tau) * d) * ratio[l]) * v3) / expm1(hv / T[l]);
+    cf[(int64_t)l * n + j] = c;
+    sum = (m == 0) ? c : sum + c;
+  }
+  for (int l = 0; l < nL; ++l) cf[(int64_t)l * n + j] = cf[(int64_t)l * n + j] / sum;
+}
+
+void launch_milne(const double* dtaus, int nL, int64_t n, const double* fp, double* out,
+                  hipStream_t st) {
+  hipLaunchKernelGGL(milne_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, dtaus,
+                     nL, n, fp, out);
+}
+
+void launch_contribution(const double* dtaus, int nL, int64_t n, const double* nu,
+                         const double* ratio, const double* T, double hcperk, double* cf,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(contribution_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     dtaus, nL, n, nu, ratio, T, hcperk, cf);
+}
+
 __global__ void fill_kernel(double* x, int64_t n, double v) {
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
        idx += (int64_t)gridDim.x * blockDim.x)

@@ -135,6 +135,7 @@ struct frei_ctx {
   SpecMeta* d_smeta_eff = nullptr;
   double* d_ones = nullptr;
   int32_t* d_prow = nullptr;
+  bool dtaus_valid = false;  // d_dtaus holds the last frei_run's final-emit dtaus
   double *d_part = nullptr, *d_Fb = nullptr, *d_Fb_all = nullptr;
   // T-P loop state
   int* d_conv = nullptr;
@@ -843,6 +844,7 @@ int frei_sweep(frei_ctx* c, int direction, double alpha, double* dT, double* bol
     TRY(ensure_dtaus(c));
     o.dtaus = c->d_dtaus;
   }
+  c->dtaus_valid = false;
   launch_setup(setup_args(c), direction, c->stream);
   HIP_TRY(hipGetLastError());
   TRY(run_sweep(c, o));
@@ -936,6 +938,7 @@ int frei_run(frei_ctx* c, const double* T_init, int n_timesteps, int n_zero_cros
   }
   // final emit without alpha (alpha = 1, core.py:323-333), writes dtaus
   TRY(ensure_dtaus(c));
+  c->dtaus_valid = true;
   SweepOpts f;
   f.dir = kEmit;
   f.force = 1;
@@ -1091,6 +1094,70 @@ int frei_comm_init_host(frei_ctx* c, int nranks, int rank, frei_allgather_fn fn,
   c->nranks = nranks;
   c->rank = rank;
   return 0;
+}
+
+// dtaus for post-processing: the caller's host array (uploaded) or the device copy.
+static int post_dtaus(frei_ctx* c, const double* h, double** tmp, const double** d) {
+  *tmp = nullptr;
+  if (h) {
+    const size_t n = (size_t)c->nL * c->nlam;
+    TRY(dalloc(tmp, n));
+    TRY(h2d(*tmp, h, n, c->stream));
+    *d = *tmp;
+    return 0;
+  }
+  if (!c->dtaus_valid || !c->d_dtaus) return fail("no device dtaus: run frei_run first or pass dtaus");
+  *d = c->d_dtaus;
+  return 0;
+}
+
+int frei_milne_pressure(frei_ctx* c, const double* dtaus, const double* p_bar,
+                        double* p_milne) {
+  if (!ready(c) || !p_bar || !p_milne) return fail("context not ready or null argument");
+  TRY(set_device(c));
+  double *tmp = nullptr, *d_fp = nullptr, *d_out = nullptr;
+  const double* d_dt = nullptr;
+  int rc = post_dtaus(c, dtaus, &tmp, &d_dt);
+  if (!rc) rc = dalloc(&d_fp, c->nL);
+  if (!rc) rc = dalloc(&d_out, c->nlam);
+  if (!rc) rc = h2d(d_fp, p_bar, c->nL, c->stream);
+  if (!rc) {
+    launch_milne(d_dt, c->nL, c->nlam, d_fp, d_out, c->stream);
+    if (hipGetLastError() != hipSuccess) rc = fail("milne kernel launch failed");
+  }
+  if (!rc && hipMemcpyAsync(p_milne, d_out, c->nlam * sizeof(double), hipMemcpyDeviceToHost,
+                            c->stream) != hipSuccess)
+    rc = fail("milne copy failed");
+  if (hipStreamSynchronize(c->stream) != hipSuccess && !rc) rc = fail("milne kernel failed");
+  dfree(tmp), dfree(d_fp), dfree(d_out);
+  return rc;
+}
+
+int frei_contribution(frei_ctx* c, const double* dtaus, const double* nu, const double* ratio,
+                      const double* T, double hcperk, double* cf) {
+  if (!ready(c) || !nu || !ratio || !T || !cf) return fail("context not ready or null argument");
+  TRY(set_device(c));
+  double *tmp = nullptr, *d_nu = nullptr, *d_ratio = nullptr, *d_T = nullptr, *d_cf = nullptr;
+  const double* d_dt = nullptr;
+  const size_t n = (size_t)c->nL * c->nlam;
+  int rc = post_dtaus(c, dtaus, &tmp, &d_dt);
+  if (!rc) rc = dalloc(&d_nu, c->nlam);
+  if (!rc) rc = dalloc(&d_ratio, c->nL);
+  if (!rc) rc = dalloc(&d_T, c->nL);
+  if (!rc) rc = dalloc(&d_cf, n);
+  if (!rc) rc = h2d(d_nu, nu, c->nlam, c->stream);
+  if (!rc) rc = h2d(d_ratio, ratio, c->nL, c->stream);
+  if (!rc) rc = h2d(d_T, T, c->nL, c->stream);
+  if (!rc) {
+    launch_contribution(d_dt, c->nL, c->nlam, d_nu, d_ratio, d_T, hcperk, d_cf, c->stream);
+    if (hipGetLastError() != hipSuccess) rc = fail("contribution kernel launch failed");
+  }
+  if (!rc && hipMemcpyAsync(cf, d_cf, n * sizeof(double), hipMemcpyDeviceToHost, c->stream) !=
+                 hipSuccess)
+    rc = fail("contribution copy failed");
+  if (hipStreamSynchronize(c->stream) != hipSuccess && !rc) rc = fail("contribution kernel failed");
+  dfree(tmp), dfree(d_nu), dfree(d_ratio), dfree(d_T), dfree(d_cf);
+  return rc;
 }
 
 int frei_ctx_path(frei_ctx* c, int* flags) {

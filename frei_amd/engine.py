@@ -236,6 +236,28 @@ class Engine:
         N.check(N.lib().frei_timing_read(self._ctx, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def milne_pressure(self, p_bar, dtaus=None):
+        """Per-wavelength Milne pressures of this slice (core.py:392-395) from ``dtaus`` (host
+        array) or, with None, the dtaus the last run left on the device."""
+        out = np.empty(self.n_lam)
+        d = None if dtaus is None else N.f64(dtaus)
+        N.check(N.lib().frei_milne_pressure(self._ctx, N.dptr(d), N.dptr(N.f64(p_bar)),
+                                            N.dptr(out)))
+        return out
+
+    def contribution(self, p_bar, T, dtaus=None):
+        """Contribution function of this slice (plot.py:63-79), rows bottom-first."""
+        p = np.asarray(p_bar, dtype=float)
+        dlogP = (np.log10(p.max()) - np.log10(p.min())) / (len(p) - 1)
+        k = 10 ** -dlogP
+        ratio = N.f64(p / ((1 - k) * p))
+        nu = N.f64(1.0 / (self.lam_um[self.lo:self.hi] * UM))
+        cf = np.empty((self.n_layers, self.n_lam))
+        d = None if dtaus is None else N.f64(dtaus)
+        N.check(N.lib().frei_contribution(self._ctx, N.dptr(d), N.dptr(nu), N.dptr(ratio),
+                                          N.dptr(N.f64(T)), H * C / K_B, N.dptr(cf)))
+        return cf
+
     def path(self):
         """Sweep implementation the tables select: dict(fast, lds_steps, contracted, nan)."""
         f = ctypes.c_int(0)

@@ -146,6 +146,23 @@ int frei_comm_init(frei_ctx* ctx, int nranks, int rank, const void* id128);
 typedef int (*frei_allgather_fn)(const double* send, double* recv, int64_t n, void* user);
 int frei_comm_init_host(frei_ctx* ctx, int nranks, int rank, frei_allgather_fn fn, void* user);
 
+/*
+ * Post-processing of a converged atmosphere (§8(f) #3), per wavelength on this slice.
+ * dtaus[n_layers][n_lam] is the host array frei_run returned, or NULL to use the copy the
+ * last frei_run left on the device.
+ *   frei_milne_pressure  core.py:392-395  p_milne[j] = np.interp(2/3, exp(-dtaus[:, j]),
+ *                        p_bar) (numpy's search, unsorted transmissions included); the
+ *                        weighted mean and final interpolation (core.py:397-405) stay on
+ *                        the host.
+ *   frei_contribution    plot.py:63-79  cf[n_layers][n_lam], rows bottom-first (cf[::-1]),
+ *                        from nu[n_lam] (cm^-1), ratio[n_layers] = p / dP, T[n_layers] and
+ *                        hcperk = h c / k_B (cm K).
+ */
+int frei_milne_pressure(frei_ctx* ctx, const double* dtaus, const double* p_bar,
+                        double* p_milne);
+int frei_contribution(frei_ctx* ctx, const double* dtaus, const double* nu,
+                      const double* ratio, const double* T, double hcperk, double* cf);
+
 /* Which sweep implementation the context's current tables select (after metadata build):
  * bit 0 fast path (on-node pressures, >= 2 T nodes, S <= 8), bit 1 step table staged in
  * LDS (shared brackets, small slices), bit 2 species-contracted table (K3), bit 3 tables

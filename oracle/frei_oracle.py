@@ -603,3 +603,59 @@ def binned_opacity(xsec, xsec_T, xsec_p, wl_hi, temperatures, pressures_bar, wl_
         for kt, a in enumerate(ti):
             out[kp, kt] = binned[where[(a, b)]]
     return out
+
+
+# ----------------------------------------------------------------- post-processing (§8(f) #3)
+# Pinned by tests/golden/post_c1.npz (the reference's effective_temperature and dashboard
+# contribution function on a converged C1 atmosphere).
+def milne_pressures(dtaus, p_bar):
+    """Per-wavelength Milne pressure (core.py:392-395): np.interp(2/3, exp(-dtaus[:, i]),
+    pressures) — numpy's interp on the (unsorted) per-layer transmissions."""
+    dtaus = np.asarray(dtaus, dtype=float)
+    return np.array([np.interp(2 / 3, np.exp(-dtaus[:, i]), p_bar)
+                     for i in range(dtaus.shape[1])])
+
+
+def effective_temperature_milne(lam_um, p_bar, spectrum, dtaus, final_T):
+    """core.py:386-405: weights = F_lambda -> erg s^-1 cm^-2 (astropy spectral_density:
+    lambda F_lambda), then interp of the weighted mean pressure on the reversed T-P
+    profile."""
+    pm = milne_pressures(dtaus, p_bar)
+    w = np.asarray(spectrum) * (np.asarray(lam_um) * 1e-4)
+    return np.interp(np.average(pm, weights=w), np.asarray(p_bar)[::-1],
+                     np.asarray(final_T)[::-1])
+
+
+def effective_temperature_planck(lam_um, spectrum):
+    """core.py:408-414: (trapz(F, lam) / sigma_SB) ** (1/4), lam in cm."""
+    lam_cm = np.asarray(lam_um) * 1e-4
+    f = np.asarray(spectrum)
+    bol = np.sum(np.diff(lam_cm) * (f[1:] + f[:-1]) / 2.0)
+    return (bol / SIGMA_SB) ** 0.25
+
+
+def effective_temperature(lam_um, p_bar, spectrum, dtaus, final_T):
+    """core.py:417-439: mean of the Milne and Stefan-Boltzmann estimates."""
+    return float(np.mean([effective_temperature_milne(lam_um, p_bar, spectrum, dtaus, final_T),
+                          effective_temperature_planck(lam_um, spectrum)]))
+
+
+def contribution_function(lam_um, p_bar, final_T, dtaus):
+    """dashboard's contribution function (plot.py:63-79) in cgs, returned as plotted
+    (cf[::-1]: rows bottom-first like the pressures):
+    tau = cumsum(dtaus[::-1]); cf = exp(-tau) * dtau * (p / dP) * nu^3 / expm1(hc nu / k T),
+    normalised over layers at every wavelength."""
+    dtaus = np.asarray(dtaus, dtype=float)
+    p = np.asarray(p_bar, dtype=float)
+    tau = np.cumsum(dtaus[::-1], axis=0)
+    nus = 1.0 / (np.asarray(lam_um) * 1e-4)
+    hcperk = H * C / K_B
+    dlogP = (np.log10(p.max()) - np.log10(p.min())) / (len(p) - 1)
+    k = 10 ** -dlogP
+    dParr = (1 - k) * p
+    T = np.asarray(final_T, dtype=float)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        cf = (np.exp(-tau) * dtaus[::-1] * (p[::-1, None] / dParr[::-1, None]) *
+              nus ** 3 / np.expm1(hcperk * nus / T[::-1, None]))
+        cf /= np.sum(cf, axis=0)
+    return cf[::-1]
