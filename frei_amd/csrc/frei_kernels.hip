@@ -256,27 +256,10 @@ struct StepCoef {
   int layer, top;
 };
 
-__device__ __forceinline__ void coef_from(double w0, double dtau, double B1, double B2,
+// Terms after E (twostream.py:143-176), same expression order as two_stream().
+__device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, double B2,
+                                          double Emw, double sq, double r, double q,
                                           StepCoef& c) {
-  // twostream.py:139-176, same order as two_stream()
-  // E = 1 where w0 <= 0.1 (twostream.py:90-94): then E * Emw, Emw / E and Bprime / (2 E)
-  // are exact without the multiply/divide, and sqrt(E * Emw) == sqrt(Emw / E), so that
-  // branch skips two divisions and a square root with bit-identical results.
-  double E, Emw, sq, r, q;
-  const double Bp = (B1 - B2) / dtau;
-  if (w0 > 0.1) {
-    E = (1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0);
-    Emw = E - w0;
-    sq = sqrt(E * Emw);
-    r = sqrt(Emw / E);
-    q = Bp / (2.0 * E);
-  } else {
-    E = 1.0;
-    Emw = 1.0 - w0;
-    sq = sqrt(Emw);
-    r = sq;
-    q = Bp * 0.5;
-  }
   const double Tr = exp((-2.0 * sq) * dtau);
   const double zp = 0.5 * (1.0 + r);
   const double zm = 0.5 * (1.0 - r);
@@ -295,12 +278,35 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
   c.dtau = dtau;
 }
 
+// General step (twostream.py:139-176): E of Deitrick 2020 Eqn 19 where w0 > 0.1, else 1.
+__device__ __forceinline__ void coef_from(double w0, double dtau, double B1, double B2,
+                                          StepCoef& c) {
+  const double E = (w0 > 0.1) ? ((1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0)) : 1.0;
+  const double Emw = E - w0;
+  const double q = ((B1 - B2) / dtau) / (2.0 * E);
+  coef_tail(w0, dtau, B1, B2, Emw, sqrt(E * Emw), sqrt(Emw / E), q, c);
+}
+
+// Step whose w0 <= 0.1 (E = 1): E * Emw, Emw / E and Bprime / (2 E) are exact without the
+// multiply/divide and sqrt(E * Emw) == sqrt(Emw / E), so this skips two divisions and a
+// square root with bit-identical results.  Taken when the whole wave qualifies.
+__device__ __forceinline__ void coef_e1(double w0, double dtau, double B1, double B2,
+                                        StepCoef& c) {
+  const double Emw = 1.0 - w0;
+  const double sq = sqrt(Emw);
+  coef_tail(w0, dtau, B1, B2, Emw, sq, sq, ((B1 - B2) / dtau) * 0.5, c);
+}
+
+struct PreCoef {
+  double w0, dtau, B1, B2;
+};
+
 template <int DIR, int S, int PD, bool NANCHK, bool SH>
 __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     FastArgs a, const FastStep* __restrict__ st, const FastStepS* __restrict__ ss,
     double* __restrict__ Fu, double* __restrict__ Fd, double* __restrict__ part,
     double* __restrict__ dtaus) {
-  static_assert(PD == 1 || PD == 2, "prefetch depth 1 or 2");
+  static_assert(PD == 1 || PD == 2 || PD == 4, "prefetch depth 1, 2 or 4");
   if (!a.force && *a.conv) return;
   extern __shared__ double red[];  // [wave][step][4], then (shared brackets) the step table
   const int tid = threadIdx.x;
@@ -370,9 +376,11 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
                                        : Fu + (int64_t)i * nl;
     stale = src[j];
   };
-  // Opacity and coefficients of step k from buffer v (then refilled with step k + PD).
+  // Phase A of step k from buffer v (then refilled with step k + PD): opacity, dtau,
+  // single-scattering albedo and the Planck terms, everything before E.
   // Bprev: emit -> B(T1) of this step, absorb -> B(T2) of this step (reuse, Q: B2 = next B1).
-  auto coef = [&](int k, double (&v)[2 * S], double& stale, double Bprev, StepCoef& c) {
+  auto coef = [&](int k, double (&v)[2 * S], double& stale, double Bprev, StepCoef& c,
+                  PreCoef& pc) {
     const int kk = k < ns ? k : ns - 1;  // the last pair of a PD = 2 loop may be a dummy
     double T1, T2, dm;
     if constexpr (SH) {
@@ -423,12 +431,35 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       B1 = planck(c1, lk, T1);
       c.Bnext = B1;
     }
+    pc.w0 = w0;
+    pc.dtau = dtau;
+    pc.B1 = B1;
+    pc.B2 = B2;
+  };
+  // Phase B for a group of steps: the E = 1 form when every lane of every step has
+  // w0 <= 0.1 (a wave-uniform branch, so the group stays one straight-line block), else the
+  // general form (bit-identical on the E = 1 lanes).
+  auto coefB = [&](PreCoef (&pc)[PD], StepCoef (&c)[PD]) {
 #ifdef FREI_MEMONLY  // diagnostic build: same memory traffic, trivial arithmetic
-    c.psi = 0.5; c.xi = w0; c.ic = 1.0; c.Xu = B2 + dtau; c.Xd = B1; c.dtau = dtau;
+#pragma unroll
+    for (int b = 0; b < PD; ++b) {
+      c[b].psi = 0.5; c[b].xi = pc[b].w0; c[b].ic = 1.0; c[b].Xu = pc[b].B2 + pc[b].dtau;
+      c[b].Xd = pc[b].B1; c[b].dtau = pc[b].dtau;
+    }
 #else
-    coef_from(w0, dtau, B1, B2, c);
+    bool e1 = true;
+#pragma unroll
+    for (int b = 0; b < PD; ++b) e1 = e1 && !(pc[b].w0 > 0.1);
+    if (__all(e1)) {
+#pragma unroll
+      for (int b = 0; b < PD; ++b) coef_e1(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2, c[b]);
+    } else {
+#pragma unroll
+      for (int b = 0; b < PD; ++b) coef_from(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2, c[b]);
+    }
 #endif
   };
+
   // Carry-dependent finish of step k: fluxes, stores, bolometric partials.
   double carry;
   auto finish = [&](int k, const StepCoef& c) {
@@ -464,26 +495,24 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       Bc = planck(c1, lk, T20);
     }
   }
-  double va[2 * S], sa;
-  load(0, va, sa);
-  if constexpr (PD == 1) {
-    for (int k = 0; k < ns; ++k) {
-      StepCoef ca;
-      coef(k, va, sa, Bc, ca);
-      Bc = ca.Bnext;
-      finish(k, ca);
+  // PD steps in flight: their loads are issued PD steps ahead, their coefficients form one
+  // block (PD-way instruction-level parallelism), then the short carried recurrence.
+  double vb[PD][2 * S], sb[PD];
+#pragma unroll
+  for (int b = 0; b < PD; ++b) load(b, vb[b], sb[b]);
+  for (int k = 0; k < ns; k += PD) {
+    StepCoef c[PD];
+    PreCoef pc[PD];
+    double Bp = Bc;
+#pragma unroll
+    for (int b = 0; b < PD; ++b) {
+      coef(k + b, vb[b], sb[b], Bp, c[b], pc[b]);
+      Bp = c[b].Bnext;
     }
-  } else {
-    double vb[2 * S], sb;
-    load(1, vb, sb);
-    for (int k = 0; k < ns; k += 2) {   // two buffers in flight, static register names
-      StepCoef ca, cb;
-      coef(k, va, sa, Bc, ca);      // both layers' coefficients: independent work
-      coef(k + 1, vb, sb, ca.Bnext, cb);
-      Bc = cb.Bnext;
-      finish(k, ca);                    // then the short carried recurrence
-      finish(k + 1, cb);
-    }
+    Bc = Bp;
+    coefB(pc, c);
+#pragma unroll
+    for (int b = 0; b < PD; ++b) finish(k + b, c[b]);
   }
   __syncthreads();
   const int nw = kBlock / 64;
@@ -1006,7 +1035,10 @@ static void launch_fast_pd(int dir, int S, const FastArgs& a, int nblocks, hipSt
 template <bool SH>
 static void launch_fast_sh(int dir, int S, int depth, bool nan_check, const FastArgs& a,
                            int nblocks, hipStream_t st) {
-  if (depth >= 2) {
+  if (depth >= 4 && S == 1 && !nan_check) {  // 4 steps in flight: small slices, one table
+    if (dir == kEmit) launch_fast_t<kEmit, 1, 4, false, SH>(a, nblocks, st);
+    else launch_fast_t<kAbsorb, 1, 4, false, SH>(a, nblocks, st);
+  } else if (depth >= 2) {
     if (nan_check) launch_fast_pd<2, true, SH>(dir, S, a, nblocks, st);
     else launch_fast_pd<2, false, SH>(dir, S, a, nblocks, st);
   } else {

@@ -155,6 +155,7 @@ struct frei_ctx {
   // FREI_SHARED=0/1 forces it off/on; FREI_SHARED_MAX_BLOCKS moves the threshold.
   int shared_mode = -1;
   int shared_max_blocks = 1024;
+  int depth4_max_blocks = 0;            // FREI_DEPTH4_MAX_BLOCKS (4 steps in flight: off, measured no faster)
   frei_allgather_fn host_ag = nullptr;  // host all-gather callback (alternative to RCCL)
   void* host_ag_user = nullptr;
   double* h_ag = nullptr;               // pinned [nranks + 1][n_steps * 4]
@@ -438,7 +439,10 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     f.conv = c->d_conv;
     // Prefetch depth: below ~2 waves per SIMD (small per-GPU slices, e.g. 500k lambda over
     // 8 GPUs) a second layer in flight hides HBM latency; at full occupancy one suffices.
-    const int depth = c->prefetch_depth > 0 ? c->prefetch_depth : 2;
+    // With one table (K3) and few blocks per CU, four steps in flight add the
+    // instruction-level parallelism that occupancy cannot (FREI_DEPTH4_MAX_BLOCKS).
+    const int depth = c->prefetch_depth > 0 ? c->prefetch_depth
+                      : (S_run == 1 && c->nblocks <= c->depth4_max_blocks) ? 4 : 2;
     bool nan_check = false;
     for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
     launch_sweep_fast(o.dir, S_run, depth, nan_check && !c->eff, c->shared != 0, f,
@@ -564,6 +568,7 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
   if (const char* e = getenv("FREI_SHARED")) c->shared_mode = atoi(e) ? 1 : 0;
   if (const char* e = getenv("FREI_SHARED_MAX_BLOCKS")) c->shared_max_blocks = atoi(e);
   if (const char* e = getenv("FREI_PRECONTRACT")) c->eff_mode = atoi(e) ? 1 : 0;
+  if (const char* e = getenv("FREI_DEPTH4_MAX_BLOCKS")) c->depth4_max_blocks = atoi(e);
   auto bail = [&](int rc) {
     frei_ctx_destroy(c);
     return rc;

@@ -58,6 +58,9 @@ def main():
         print(f"{name:>14s}: sweep median {med:.4f} ms  min {min(res):.4f} ms  "
               f"{bpu * (w['p'].size - 1) * n_lam / (min(res) * 1e-3) / 1e12:.3f} TB/s algorithmic "
               f"({n_lam} lambda, {S} species)")
+    for name, lib, eng, res in builds:   # close every context with its own library
+        N._lib = lib
+        eng.close()
 
 
 if __name__ == "__main__":
