@@ -523,6 +523,206 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   }
 }
 
+// ---------------------------------------------------------------- K1, paired-lane form
+// Small slices (e.g. 62.5k lambda per GPU over 8 GPUs) leave about one wave per SIMD, and a
+// lone wave issues a vector instruction only every other slot.  This form spends two lanes
+// per wavelength so the same slice runs twice the waves: lane pair (2m, 2m+1) owns
+// wavelength m of the wave's 32, and within each group of two sweep steps the even lane
+// computes step k's coefficients and the odd lane step k+1's (one instruction stream for
+// both).  The carried recurrence then runs through the pair in order (carry broadcast by
+// DPP), each lane stores its own step, and the bolometric terms of the two steps are
+// reduced together over the 32 lanes of each parity (5 exchanges for 8 sums).  Fluxes are
+// formed by the same expressions in the same order as the one-lane form (bit-identical);
+// the bolometric partial sums use this form's own fixed summation tree.  One contracted
+// table (K3), step table staged in LDS.
+template <int CTRL>
+__device__ __forceinline__ double dpp_bcast(double x) {
+  const int2 v = __builtin_bit_cast(int2, x);
+  int2 r;
+  r.x = __builtin_amdgcn_mov_dpp(v.x, CTRL, 0xF, 0xF, false);
+  r.y = __builtin_amdgcn_mov_dpp(v.y, CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, r);
+}
+constexpr int kQpEven = 0xA0;  // quad_perm [0,0,2,2]: each pair reads its even lane
+constexpr int kQpOdd = 0xF5;   // quad_perm [1,1,3,3]: each pair reads its odd lane
+constexpr int kQpSwap = 0xB1;  // quad_perm [1,0,3,2]: partner lane
+
+// Sums of q0..q3 over the 32 lanes of each parity (lane bit 0).  Lane h + 2b + 4c ends
+// with the sum of q[2b + c] over the lanes of parity h.  Fixed order: deterministic.
+__device__ __forceinline__ double pair_sum4(double q0, double q1, double q2, double q3,
+                                            int lane) {
+  const bool b = lane & 2;
+  const double r0 = __shfl_xor(b ? q0 : q2, 2, 64);
+  const double r1 = __shfl_xor(b ? q1 : q3, 2, 64);
+  const double x0 = (b ? q2 : q0) + r0;
+  const double x1 = (b ? q3 : q1) + r1;
+  const bool c = lane & 4;
+  double y = (c ? x1 : x0) + __shfl_xor(c ? x0 : x1, 4, 64);
+#pragma unroll
+  for (int o = 8; o <= 32; o <<= 1) y += __shfl_xor(y, o, 64);
+  return y;
+}
+
+template <int DIR>
+__global__ __launch_bounds__(kBlock) void sweep_pair_kernel(
+    FastArgs a, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
+    double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
+  if (!a.force && *a.conv) return;
+  extern __shared__ double red[];  // [wave][step][4], then the step table
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int h = lane & 1;          // step parity this lane computes
+  const int64_t nl = a.n_lam;
+  const int64_t j0 = (int64_t)blockIdx.x * (kBlock / 2) + wv * 32 + (lane >> 1);
+  const bool act = j0 < nl;
+  const int64_t j = act ? j0 : nl - 1;
+  const double c1 = a.c1[j], lk = a.lk[j], sig = a.sig[j];
+  const double wt = act ? a.wtr[j] : 0.0;
+  const int ns = a.n_steps;
+  const double* __restrict__ tab = a.tab[0];
+  double* lss = red + (int64_t)(kBlock / 64) * ns * 4;
+  {
+    const double* g = reinterpret_cast<const double*>(ss);
+    constexpr int kW = sizeof(FastStepS) / sizeof(double);
+    for (int idx = tid; idx < ns * kW; idx += kBlock) lss[idx] = g[idx];
+    __syncthreads();
+  }
+  const FastStepS* sp = reinterpret_cast<const FastStepS*>(lss);
+  auto clampk = [&](int k) { return k < ns ? k : ns - 1; };
+  // loads of this lane's step in group g (step 2g + h, clamped for a dummy step)
+  auto load = [&](int g, double& vlo, double& vhi, double& stale) {
+    const int k = clampk(2 * g + h);
+    const double* r = tab + sp[k].off + j;
+    vlo = stream_load(r);
+    vhi = stream_load(r + a.pitch);
+    const int layer = sp[k].layer;
+    const double* src = (DIR == kEmit) ? (sp[k].top ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
+                                       : Fu + (int64_t)layer * nl;
+    stale = src[j];
+  };
+  double carry, carryB;
+  {
+    const int l0 = sp[0].layer;
+    if (DIR == kEmit) {
+      carry = Fu[(int64_t)l0 * nl + j];
+      carryB = planck(c1, lk, sp[0].T1);
+    } else {
+      carry = Fd[(int64_t)(l0 + 1) * nl + j];
+      carryB = planck(c1, lk, sp[0].T2);
+    }
+  }
+  // Phase A of this lane's step in group g (opacity, dtau, albedo, Planck chain of the
+  // pair); refills the group's buffer with group g + 2.
+  struct PairA {
+    double w0, dtau, B1, B2, F_st;
+    int k;
+  };
+  auto phaseA = [&](int g, double& vlo, double& vhi, double& stale, PairA& A) {
+    const int k = 2 * g + h;
+    const FastStepS& st = sp[clampk(k)];
+    A.k = k;
+    A.F_st = stale;
+    const double kap = st.mmr[0] * ((0.0 + vlo * st.wlo) + vhi * st.whi) + sig;
+    load(g + 2, vlo, vhi, stale);
+    A.dtau = st.dm * kap;
+    A.w0 = sig / (sig + kap);
+    // each lane forms its step's new Planck value; the pair exchanges them and both lanes
+    // resolve (B1, B2) of both steps in order (emit: B2 is new and becomes the next B1;
+    // absorb: B1 is new and becomes the next B2)
+    const double X = planck(c1, lk, DIR == kEmit ? st.T2 : st.T1);
+    const double Xo = dpp_bcast<kQpSwap>(X);
+    const double X0 = h ? Xo : X, X1 = h ? X : Xo;
+    const bool top0 = sp[clampk(2 * g)].top, top1 = sp[clampk(2 * g + 1)].top;
+    const double Bn0 = (DIR == kEmit && top0) ? carryB : X0;
+    const double Bn1 = (DIR == kEmit && top1) ? Bn0 : X1;
+    if (DIR == kEmit) {
+      A.B1 = h ? Bn0 : carryB;
+      A.B2 = h ? Bn1 : Bn0;
+    } else {
+      A.B2 = h ? Bn0 : carryB;
+      A.B1 = h ? X1 : X0;
+    }
+    carryB = Bn1;
+  };
+  // Carried recurrence through the pair (the even lane's step, then the odd lane's),
+  // stores of this lane's step and the reduction of the pair's bolometric terms.
+  auto finish = [&](const PairA& A, const StepCoef& c) {
+    const double F_st = A.F_st;
+    const double mid0 = carry;
+    double F2u_a, F1d_a, F2u_b, F1d_b;
+    {
+      double F1u, F2d;
+      if (DIR == kEmit) { F1u = mid0; F2d = F_st; } else { F2d = mid0; F1u = F_st; }
+      F2u_a = c.ic * ((c.psi * F1u - c.xi * F2d) + c.Xu);
+      F1d_a = c.ic * ((c.psi * F2d - c.xi * F1u) + c.Xd);
+    }
+    const double mid = dpp_bcast<kQpEven>(DIR == kEmit ? F2u_a : F1d_a);
+    {
+      double F1u, F2d;
+      if (DIR == kEmit) { F1u = mid; F2d = F_st; } else { F2d = mid; F1u = F_st; }
+      F2u_b = c.ic * ((c.psi * F1u - c.xi * F2d) + c.Xu);
+      F1d_b = c.ic * ((c.psi * F2d - c.xi * F1u) + c.Xd);
+    }
+    carry = dpp_bcast<kQpOdd>(DIR == kEmit ? F2u_b : F1d_b);
+    const double cin = h ? mid : mid0;
+    const double F2u = h ? F2u_b : F2u_a, F1d = h ? F1d_b : F1d_a;
+    const double F1u = (DIR == kEmit) ? cin : F_st;
+    const double F2d = (DIR == kEmit) ? F_st : cin;
+    const int k = A.k;
+    if (act && k < ns) {
+      const FastStepS& st = sp[k];
+      const int i = st.layer;
+      const bool st_up = (DIR == kEmit) ? !st.top : (!a.live_only || i == 0);
+      const bool st_dn = (DIR == kAbsorb) || !a.live_only || st.top;
+      if (st_up) Fu[(int64_t)(i + 1) * nl + j] = F2u;
+      if (st_dn) Fd[(int64_t)i * nl + j] = F1d;
+      if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = c.dtau;
+    }
+    const double y = pair_sum4(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
+    const int kq = (k - h) + (lane & 1);
+    if (lane < 8 && kq < ns)
+      red[((int64_t)wv * ns + kq) * 4 + ((lane >> 1) & 1) * 2 + ((lane >> 2) & 1)] = y;
+  };
+  const int ng = (ns + 1) / 2;
+  double la, ha, sa, lb, hb, sb;   // two groups (four steps) in flight
+  load(0, la, ha, sa);
+  load(1, lb, hb, sb);
+  for (int g = 0; g < ng; g += 2) {
+    PairA A0, A1;
+    phaseA(g, la, ha, sa, A0);
+    phaseA(g + 1, lb, hb, sb, A1);   // a dummy group past the end is computed, not stored
+    StepCoef c0, c1;
+    if (__all(!(A0.w0 > 0.1) && !(A1.w0 > 0.1))) {
+      coef_e1(A0.w0, A0.dtau, A0.B1, A0.B2, c0);
+      coef_e1(A1.w0, A1.dtau, A1.B1, A1.B2, c1);
+    } else {
+      coef_from(A0.w0, A0.dtau, A0.B1, A0.B2, c0);
+      coef_from(A1.w0, A1.dtau, A1.B1, A1.B2, c1);
+    }
+    finish(A0, c0);
+    if (g + 1 < ng) finish(A1, c1);
+  }
+  __syncthreads();
+  const int nw = kBlock / 64;
+  for (int idx = tid; idx < ns * 4; idx += kBlock) {
+    double s = red[idx];
+    for (int w = 1; w < nw; ++w) s += red[(int64_t)w * ns * 4 + idx];
+    part[(int64_t)idx * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+void launch_sweep_pair(int dir, const FastArgs& a, int nblocks, hipStream_t st) {
+  const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double) +
+                     (size_t)a.n_steps * sizeof(FastStepS);
+  if (dir == kEmit)
+    hipLaunchKernelGGL(sweep_pair_kernel<kEmit>, dim3(nblocks), dim3(kBlock), shm, st, a,
+                       a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+  else
+    hipLaunchKernelGGL(sweep_pair_kernel<kAbsorb>, dim3(nblocks), dim3(kBlock), shm, st, a,
+                       a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+}
+
 // ---------------------------------------------------------------- partial sums
 __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ part,
                                                      int nblocks, double* __restrict__ Fb,

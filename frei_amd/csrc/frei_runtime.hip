@@ -155,6 +155,9 @@ struct frei_ctx {
   // FREI_SHARED=0/1 forces it off/on; FREI_SHARED_MAX_BLOCKS moves the threshold.
   int shared_mode = -1;
   int shared_max_blocks = 1024;
+  // Paired-lane sweep (two lanes per wavelength): contracted table, LDS step table and at
+  // most this many 256-wavelength blocks, i.e. about one wave per SIMD or less.
+  int pair_max_blocks = 1024;           // FREI_PAIR_MAX_BLOCKS (<= 262k lambda per GPU)
   int depth4_max_blocks = 0;            // FREI_DEPTH4_MAX_BLOCKS (4 steps in flight: off, measured no faster)
   frei_allgather_fn host_ag = nullptr;  // host all-gather callback (alternative to RCCL)
   void* host_ag_user = nullptr;
@@ -415,6 +418,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     if (!e0 || !e1) return fail("hipEventCreate failed");
     HIP_TRY(hipEventRecord(e0, c->stream));
   }
+  int nb_run = c->nblocks;  // partial-sum columns written by this sweep
   if (c->fast) {
     FastArgs f{};
     f.n_lam = c->nlam;
@@ -445,14 +449,19 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
                       : (S_run == 1 && c->nblocks <= c->depth4_max_blocks) ? 4 : 2;
     bool nan_check = false;
     for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
-    launch_sweep_fast(o.dir, S_run, depth, nan_check && !c->eff, c->shared != 0, f,
-                      c->nblocks, c->stream);
+    if (c->eff && c->shared && c->nblocks <= c->pair_max_blocks) {
+      nb_run = (int)((c->nlam + kBlock / 2 - 1) / (kBlock / 2));
+      launch_sweep_pair(o.dir, f, nb_run, c->stream);
+    } else {
+      launch_sweep_fast(o.dir, S_run, depth, nan_check && !c->eff, c->shared != 0, f,
+                        c->nblocks, c->stream);
+    }
   } else {
     launch_sweep(o.dir, a, c->nblocks, false, c->stream);
   }
   HIP_TRY(hipGetLastError());
   if (c->timing) HIP_TRY(hipEventRecord(e1, c->stream));
-  launch_reduce(c->d_part, c->nblocks, c->d_Fb, ns * 4, c->d_conv, o.force, c->stream);
+  launch_reduce(c->d_part, nb_run, c->d_Fb, ns * 4, c->d_conv, o.force, c->stream);
   HIP_TRY(hipGetLastError());
   const double* Fb = c->d_Fb;
   if (c->nranks > 1 && c->host_ag) {
@@ -569,6 +578,7 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
   if (const char* e = getenv("FREI_SHARED_MAX_BLOCKS")) c->shared_max_blocks = atoi(e);
   if (const char* e = getenv("FREI_PRECONTRACT")) c->eff_mode = atoi(e) ? 1 : 0;
   if (const char* e = getenv("FREI_DEPTH4_MAX_BLOCKS")) c->depth4_max_blocks = atoi(e);
+  if (const char* e = getenv("FREI_PAIR_MAX_BLOCKS")) c->pair_max_blocks = atoi(e);
   auto bail = [&](int rc) {
     frei_ctx_destroy(c);
     return rc;
@@ -587,7 +597,7 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
       (rc = dalloc(&c->d_bol, NL * 4)) || (rc = dalloc(&c->d_mmr, NS * NL)) ||
       (rc = dalloc(&c->d_steps, ns)) || (rc = dalloc(&c->d_terms, ns * NS)) ||
       (rc = dalloc(&c->d_fsteps, ns)) || (rc = dalloc(&c->d_ssteps, ns)) ||
-      (rc = dalloc(&c->d_part, ns * 4 * (size_t)c->nblocks)) ||
+      (rc = dalloc(&c->d_part, ns * 4 * (size_t)(2 * c->nblocks))) ||
       (rc = dalloc(&c->d_Fb, ns * 4)) || (rc = dalloc(&c->d_Fb_all, ns * 4)) ||
       (rc = dalloc(&c->d_conv, 1)) || (rc = dalloc(&c->d_iter, 1)) ||
       (rc = dalloc(&c->d_Tb, NL)) || (rc = dalloc(&c->d_Ta, NL)) ||
@@ -1171,7 +1181,9 @@ int frei_ctx_path(frei_ctx* c, int* flags) {
   TRY(build_meta(c));
   int nan = 0;
   for (const auto& q : c->sp) nan = nan || q.has_nan;
-  *flags = (c->fast ? 1 : 0) | (c->fast && c->shared ? 2 : 0) | (c->eff ? 4 : 0) | (nan ? 8 : 0);
+  const bool pair = c->fast && c->eff && c->shared && c->nblocks <= c->pair_max_blocks;
+  *flags = (c->fast ? 1 : 0) | (c->fast && c->shared ? 2 : 0) | (c->eff ? 4 : 0) |
+           (nan ? 8 : 0) | (pair ? 16 : 0);
   return 0;
 }
 
