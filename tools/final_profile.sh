@@ -12,3 +12,7 @@ python3 tools/pmc_valu.py gpurun_out/final/pmc_sq profiles/valu_sweep.json
 cp profiles/traffic_sweep.json profiles/valu_sweep.json gpurun_out/final/
 timeout -k 10 400 python3 bench.py > gpurun_out/final/bench.json 2> gpurun_out/final/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/final/prof -o run -- python3 bench.py --no-cpu-baseline > gpurun_out/final/bench_under_rocprof.json 2> gpurun_out/final/bench_under_rocprof.err
+# per-GPU slice sizes of the 2/4/8-GPU runs on one GPU (sweep + fixed per-sweep costs)
+for n in 250000 125000 62500; do
+  timeout -k 10 120 python3 bench.py --n-lam $n --steps 20 --no-binning --no-cpu-baseline > gpurun_out/final/bench_n$n.json 2>/dev/null
+done
