@@ -5,6 +5,7 @@ species-summed opacity assembly, radiative-equilibrium T-P loop): the public nam
 ``frei`` below keep their signatures; the compute runs in hand-written HIP kernels
 (``frei_amd/csrc``) behind the C ABI of ``include/frei_hip.h``.
 """
+from .batch import BatchEngine, batched_emission_spectra
 from .binning import BinnedTable, CrossSection, open_cross_section
 from .chemistry import chemistry, iso_to_mass, iso_to_species
 from .core import (B_star, F_TOA, Grid, Planet, Spectrum, contribution_function,
@@ -23,4 +24,5 @@ __all__ = ["Planet", "Grid", "Spectrum", "effective_temperature", "wavelength_gr
            "binned_opacity", "rayleigh_H2", "rayleigh_He", "chemistry", "iso_to_species",
            "iso_to_mass", "pressure_grid", "temperature_grid", "propagate_fluxes", "emit",
            "absorb", "BB", "E", "Engine", "partition", "trapz_weights", "CrossSection",
-           "BinnedTable", "open_cross_section", "contribution_function"]
+           "BinnedTable", "open_cross_section", "contribution_function", "BatchEngine",
+           "batched_emission_spectra"]

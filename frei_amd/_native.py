@@ -31,6 +31,11 @@ SIGNATURES = {
     "frei_ctx_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int, _i64,
                                        ctypes.c_int]),
     "frei_ctx_destroy": (ctypes.c_int, [_vp]),
+    "frei_ctx_create_batch": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int,
+                                             _i64, ctypes.c_int, ctypes.c_int]),
+    "frei_set_gravity": (ctypes.c_int, [_vp, _dp]),
+    "frei_run_batch": (ctypes.c_int, [_vp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                      ctypes.c_double, _ip, _dp, _dp]),
     "frei_set_grid": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, ctypes.c_double,
                                      ctypes.c_double]),
     "frei_set_table": (ctypes.c_int, [_vp, ctypes.c_int, _dp, _dp, ctypes.c_int, _dp,

@@ -167,6 +167,21 @@ __host__ __device__ inline void fast_term(const SpecMeta& sm, const PMeta& pm,
   whi = (1.0 * wp) * yt;
 }
 
+// Per-atmosphere element strides of the batched engine (one context holding n_atm
+// atmospheres on a shared wavelength/pressure grid and shared opacity tables, each with its
+// own temperatures, gravity, mixing ratios and fluxes; §8(f) #2).  All zero (and g null)
+// for a single atmosphere, so every kernel's atmosphere view is the identity there.
+struct AtmStride {
+  int64_t layers;    // [n_layers] state: T, Tb, Ta, flips, prev sign, n diffs
+  int64_t steps;     // step tables [n_layers - 1]
+  int64_t fb;        // reduced bolometric partials [n_steps * 4]
+  int64_t hist;      // T history [hist_cap][2][n_layers]
+  int64_t flux;      // F_up / F_down / dtaus [n_layers][n_lam]
+  int64_t tab;       // contracted opacity table
+  int64_t part;      // block partial sums [n_steps * 4][blocks]
+  const double* g;   // per-atmosphere gravity (nullptr: SetupArgs.g)
+};
+
 struct SetupArgs {
   int n_layers, n_species, fast;
   int n_tnodes;            // total sorted T nodes over species (tnodes length)
@@ -183,6 +198,7 @@ struct SetupArgs {
   FastStep* fsteps;        // [n_layers - 1] (fast path)
   FastStepS* ssteps;       // [n_layers - 1] (fast path, shared brackets)
   int shared;              // all species share p and T nodes
+  AtmStride bs;            // batched atmospheres (blockIdx.x of setup/update kernels)
 };
 
 struct FastArgs {
@@ -199,6 +215,8 @@ struct FastArgs {
   double* dtaus;
   double* part;
   const int* conv;
+  AtmStride bs;            // batched atmospheres (blockIdx.y of the sweep kernels)
+  int n_atm;               // atmospheres in the launch (0 or 1: a single atmosphere)
 };
 
 struct SweepArgs {
@@ -239,10 +257,11 @@ void launch_sweep_fast(int dir, int S, int depth, bool nan_check, bool shared,
 void launch_sweep_pair(int dir, const FastArgs& a, int nblocks, hipStream_t st);
 void launch_nan_scan(const double* x, int64_t n, int* flag, hipStream_t st);
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
-                   int force, hipStream_t st);
-void launch_setup(const SetupArgs& u, int dir, hipStream_t st);
+                   int force, hipStream_t st, int n_atm = 1, int64_t part_stride = 0,
+                   int64_t fb_stride = 0);
+void launch_setup(const SetupArgs& u, int dir, hipStream_t st, int n_atm = 1);
 void launch_log_ratio(const double* p, double p_top2, int nL, double* lnp, hipStream_t st);
-void launch_update(const UpdateArgs& a, hipStream_t st);
+void launch_update(const UpdateArgs& a, hipStream_t st, int n_atm = 1);
 void launch_propagate(int64_t n, const double* c1, const double* lk, const double* F1u,
                       const double* F2d, double T1, double T2, const double* dtau,
                       const double* w0, double* F2u, double* F1d, hipStream_t st);
@@ -257,6 +276,9 @@ void launch_milne(const double* dtaus, int nL, int64_t n, const double* fp, doub
 void launch_contribution(const double* dtaus, int nL, int64_t n, const double* nu,
                          const double* ratio, const double* T, double hcperk, double* cf,
                          hipStream_t st);
+void launch_contract_batch(const double* const* tabs, int S, const double* mmr,
+                           const int32_t* prow, int n_layers, int n_T, int64_t pitch,
+                           int n_atm, int64_t tab_stride, double* eff, hipStream_t st);
 void launch_contract(const double* const* tabs, int S, const double* mmr, const int32_t* prow,
                      int n_layers, int n_T, int64_t pitch, double* eff, hipStream_t st);
 

@@ -307,6 +307,17 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     double* __restrict__ Fu, double* __restrict__ Fd, double* __restrict__ part,
     double* __restrict__ dtaus) {
   static_assert(PD == 1 || PD == 2 || PD == 4, "prefetch depth 1, 2 or 4");
+  {  // atmosphere of a batched launch (identity for one atmosphere)
+    const int m = blockIdx.y;
+    Fu += m * a.bs.flux;
+    Fd += m * a.bs.flux;
+    part += m * a.bs.part;
+    if (dtaus) dtaus += m * a.bs.flux;
+    st += m * a.bs.steps;
+    ss += m * a.bs.steps;
+    a.tab[0] += m * a.bs.tab;
+    a.conv += m;
+  }
   if (!a.force && *a.conv) return;
   extern __shared__ double red[];  // [wave][step][4], then (shared brackets) the step table
   const int tid = threadIdx.x;
@@ -567,6 +578,16 @@ template <int DIR>
 __global__ __launch_bounds__(kBlock) void sweep_pair_kernel(
     FastArgs a, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
     double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
+  {  // atmosphere of a batched launch (identity for one atmosphere)
+    const int m = blockIdx.y;
+    Fu += m * a.bs.flux;
+    Fd += m * a.bs.flux;
+    part += m * a.bs.part;
+    if (dtaus) dtaus += m * a.bs.flux;
+    ss += m * a.bs.steps;
+    a.tab[0] += m * a.bs.tab;
+    a.conv += m;
+  }
   if (!a.force && *a.conv) return;
   extern __shared__ double red[];  // [wave][step][4], then the step table
   const int tid = threadIdx.x;
@@ -716,17 +737,23 @@ void launch_sweep_pair(int dir, const FastArgs& a, int nblocks, hipStream_t st) 
   const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double) +
                      (size_t)a.n_steps * sizeof(FastStepS);
   if (dir == kEmit)
-    hipLaunchKernelGGL(sweep_pair_kernel<kEmit>, dim3(nblocks), dim3(kBlock), shm, st, a,
+    hipLaunchKernelGGL(sweep_pair_kernel<kEmit>, dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1),
+                       dim3(kBlock), shm, st, a,
                        a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
   else
-    hipLaunchKernelGGL(sweep_pair_kernel<kAbsorb>, dim3(nblocks), dim3(kBlock), shm, st, a,
+    hipLaunchKernelGGL(sweep_pair_kernel<kAbsorb>, dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1),
+                       dim3(kBlock), shm, st, a,
                        a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
 }
 
 // ---------------------------------------------------------------- partial sums
 __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ part,
                                                      int nblocks, double* __restrict__ Fb,
-                                                     const int* conv, int force) {
+                                                     const int* conv, int force,
+                                                     int64_t part_stride, int64_t fb_stride) {
+  part += blockIdx.y * part_stride;   // atmosphere of a batched launch
+  Fb += blockIdx.y * fb_stride;
+  conv += blockIdx.y;
   if (!force && *conv) return;
   __shared__ double sh[4];
   const double* p = part + (int64_t)blockIdx.x * nblocks;
@@ -831,7 +858,33 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
   }
 }
 
+// Atmosphere m of a batched context: per-atmosphere state pointers and gravity.
+__device__ inline void atm_view(SetupArgs& u, int m) {
+  u.T += m * u.bs.layers;
+  u.steps += m * u.bs.steps;
+  u.fsteps += m * u.bs.steps;
+  u.ssteps += m * u.bs.steps;
+  if (u.bs.g) u.g = u.bs.g[m];
+}
+
+__device__ inline void atm_view(UpdateArgs& a, int m) {
+  atm_view(a.su, m);
+  const AtmStride& b = a.su.bs;
+  a.Fb += m * b.fb;
+  a.Tb += m * b.layers;
+  a.Ta += m * b.layers;
+  a.hist += m * b.hist;
+  a.flips += m * b.layers;
+  a.prev_sign += m * b.layers;
+  a.ndiff += m * b.layers;
+  a.iter += m;
+  a.conv += m;
+  if (a.dT_out) a.dT_out += m * b.layers;
+  if (a.bol_out) a.bol_out += m * b.layers * 4;
+}
+
 __global__ void setup_kernel(SetupArgs u, int dir) {
+  atm_view(u, blockIdx.x);
   setup_sweep(u, u.T, u.p, u.tnodes, u.spec, u.pmeta, u.mmr, dir);
 }
 
@@ -881,6 +934,7 @@ __host__ __device__ inline size_t update_lds_bytes(int nL, int ntn, int S, bool 
 }
 
 __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
+  atm_view(a, blockIdx.x);  // identity for one atmosphere
   if (!a.force && *a.conv) return;
   extern __shared__ __attribute__((aligned(16))) double sh[];
   __shared__ int all_conv;
@@ -1181,6 +1235,81 @@ void launch_contribution(const double* dtaus, int nL, int64_t n, const double* n
                      dtaus, nL, n, nu, ratio, T, hcperk, cf);
 }
 
+// K7: batched species contraction on fp64 MFMA (§8(f) #2).  A batched context holds n_atm
+// atmospheres, each with its own mixing ratios, on shared tables.  For every layer l
+// (pressure row prow_l) and every column c of that row's [n_T][pitch] block:
+//   eff[m][prow_l][c] = sum_s mmr[m][s][l] * tab_s[prow_l][c],
+// i.e. per layer the dense product [n_atm x S] . [S x n_T*pitch].  v_mfma_f64_16x16x4f64:
+// A = 16 atmospheres x 4 species (mixing ratios), B = 4 species x 16 columns (table values),
+// D = 16 atmospheres x 16 columns; K = S in steps of 4.  Each wave owns 16 columns for all
+// atmosphere tiles, so every table value is read once from HBM.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+struct ContractBatchArgs {
+  const double* tab[kMaxFastS];
+  const double* mmr;      // [n_atm][S][n_layers]
+  const int32_t* prow;    // [n_layers]
+  double* eff;            // [n_atm] x tab_stride
+  int S, n_layers, n_T, n_atm;
+  int64_t pitch, tab_stride;
+};
+
+__global__ __launch_bounds__(256) void contract_batch_kernel(ContractBatchArgs a) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l = blockIdx.y;
+  const int64_t ncol = (int64_t)a.n_T * a.pitch;
+  const int64_t col0 = ((int64_t)blockIdx.x * 4 + wv) * 16;
+  if (col0 >= ncol) return;
+  const int64_t rowbase = (int64_t)a.prow[l] * ncol;
+  const int ci = lane & 15, kq = lane >> 4;   // column in the tile, species in the K step
+  const int64_t col = col0 + ci;
+  const bool colok = col < ncol;
+  constexpr int kSteps = kMaxFastS / 4;
+  double b[kSteps];
+#pragma unroll
+  for (int ks = 0; ks < kSteps; ++ks) {
+    const int s = 4 * ks + kq;
+    b[ks] = (s < a.S && colok) ? a.tab[s][rowbase + col] : 0.0;
+  }
+  for (int m0 = 0; m0 < a.n_atm; m0 += 16) {
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    const int am = m0 + ci;                     // A operand row: atmosphere
+#pragma unroll
+    for (int ks = 0; ks < kSteps; ++ks) {
+      if (4 * ks >= a.S) break;
+      const int s = 4 * ks + kq;
+      const double av =
+          (am < a.n_atm && s < a.S) ? a.mmr[((int64_t)am * a.S + s) * a.n_layers + l] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[ks], acc, 0, 0, 0);
+    }
+    // D: this lane holds rows kq + 4 r (atmospheres) of column ci
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + kq + 4 * r;
+      if (m < a.n_atm && colok) a.eff[(int64_t)m * a.tab_stride + rowbase + col] = acc[r];
+    }
+  }
+}
+
+void launch_contract_batch(const double* const* tabs, int S, const double* mmr,
+                           const int32_t* prow, int n_layers, int n_T, int64_t pitch,
+                           int n_atm, int64_t tab_stride, double* eff, hipStream_t st) {
+  ContractBatchArgs a{};
+  for (int s = 0; s < S && s < kMaxFastS; ++s) a.tab[s] = tabs[s];
+  a.mmr = mmr;
+  a.prow = prow;
+  a.eff = eff;
+  a.S = S;
+  a.n_layers = n_layers;
+  a.n_T = n_T;
+  a.n_atm = n_atm;
+  a.pitch = pitch;
+  a.tab_stride = tab_stride;
+  const int64_t ncol = (int64_t)n_T * pitch;
+  dim3 grid((unsigned)((ncol + 63) / 64), (unsigned)n_layers);
+  hipLaunchKernelGGL(contract_batch_kernel, grid, dim3(256), 0, st, a);
+}
+
 __global__ void fill_kernel(double* x, int64_t n, double v) {
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
        idx += (int64_t)gridDim.x * blockDim.x)
@@ -1208,7 +1337,8 @@ template <int DIR, int S, int PD, bool NC, bool SH>
 static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
   const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double) +
                      (SH ? (size_t)a.n_steps * sizeof(FastStepS) : 0);
-  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC, SH>), dim3(nblocks), dim3(kBlock), shm,
+  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC, SH>),
+                     dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1), dim3(kBlock), shm,
                      st, a, a.steps, a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
 }
 
@@ -1266,19 +1396,20 @@ void launch_nan_scan(const double* x, int64_t n, int* flag, hipStream_t st) {
 }
 
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
-                   int force, hipStream_t st) {
-  hipLaunchKernelGGL(reduce_kernel, dim3(n_idx), dim3(256), 0, st, part, nblocks, Fb, conv,
-                     force);
+                   int force, hipStream_t st, int n_atm, int64_t part_stride,
+                   int64_t fb_stride) {
+  hipLaunchKernelGGL(reduce_kernel, dim3(n_idx, n_atm), dim3(256), 0, st, part, nblocks, Fb,
+                     conv, force, part_stride, fb_stride);
 }
 
-void launch_setup(const SetupArgs& u, int dir, hipStream_t st) {
-  hipLaunchKernelGGL(setup_kernel, dim3(1), dim3(256), 0, st, u, dir);
+void launch_setup(const SetupArgs& u, int dir, hipStream_t st, int n_atm) {
+  hipLaunchKernelGGL(setup_kernel, dim3(n_atm), dim3(256), 0, st, u, dir);
 }
 
-void launch_update(const UpdateArgs& a, hipStream_t st) {
+void launch_update(const UpdateArgs& a, hipStream_t st, int n_atm) {
   const size_t shm = update_lds_bytes(a.su.n_layers, a.su.n_tnodes, a.su.n_species,
                                       a.meta_in_lds != 0);
-  hipLaunchKernelGGL(update_kernel, dim3(1), dim3(256), shm, st, a);
+  hipLaunchKernelGGL(update_kernel, dim3(n_atm), dim3(256), shm, st, a);
 }
 
 void launch_propagate(int64_t n, const double* c1, const double* lk, const double* F1u,

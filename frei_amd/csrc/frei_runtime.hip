@@ -136,6 +136,12 @@ struct frei_ctx {
   double* d_ones = nullptr;
   int32_t* d_prow = nullptr;
   bool dtaus_valid = false;  // d_dtaus holds the last frei_run's final-emit dtaus
+  // Batched atmospheres (frei_ctx_create_batch): n_atm atmospheres share the wavelength and
+  // pressure grids and the opacity tables; every per-atmosphere buffer is n_atm blocks.
+  int n_atm = 1;
+  double* d_g = nullptr;      // [n_atm] gravity (batched)
+  size_t eff_stride = 0;      // elements per atmosphere of d_eff
+  int* h_conv = nullptr;      // pinned [2][n_atm] convergence flags (frei_run_batch)
   double *d_part = nullptr, *d_Fb = nullptr, *d_Fb_all = nullptr;
   // T-P loop state
   int* d_conv = nullptr;
@@ -198,7 +204,8 @@ int h2d(T* d, const T* h, size_t n, hipStream_t st) {
 // table holds a NaN (the reference's nansum, Q8, is per species) and S >= 2.
 int build_contracted(frei_ctx* c, bool shared_fast) {
   const int nL = c->nL, S = c->S;
-  bool on = shared_fast && S >= 2 && c->eff_mode != 0;
+  const bool batch = c->n_atm > 1;
+  bool on = shared_fast && (S >= 2 || batch) && (c->eff_mode != 0 || batch);
   for (int s = 0; s < S && on; ++s) on = !c->sp[s].has_nan;
   std::vector<int32_t> prow(nL, 0);
   if (on) {
@@ -207,22 +214,30 @@ int build_contracted(frei_ctx* c, bool shared_fast) {
       const PMeta& pm = c->pmeta[l];  // species 0 (shared nodes)
       prow[l] = (pm.wp_lo != 0.0) ? pm.p_lo : pm.p_hi;
       if (owner[prow[l]] >= 0) {  // two layers on one pressure row: mmr must agree
-        for (int s = 0; s < S && on; ++s)
-          on = c->mmr[(size_t)s * nL + l] == c->mmr[(size_t)s * nL + owner[prow[l]]];
+        for (size_t m = 0; m < (size_t)c->n_atm && on; ++m)
+          for (int s = 0; s < S && on; ++s)
+            on = c->mmr[(m * S + s) * nL + l] == c->mmr[(m * S + s) * nL + owner[prow[l]]];
       }
       owner[prow[l]] = l;
     }
   }
   c->eff = on ? 1 : 0;
-  if (!on) return 0;
+  if (!on) {
+    if (batch)
+      return fail("a batched context needs tables on shared on-node p/T nodes without NaN "
+                  "(one contracted table per atmosphere)");
+    return 0;
+  }
   const Species& q0 = c->sp[0];
-  const size_t need = (size_t)q0.n_p * q0.n_T * (size_t)q0.stride + 64;
+  const size_t per = (size_t)q0.n_p * q0.n_T * (size_t)q0.stride + 64;
+  const size_t need = per * c->n_atm;
   if (c->eff_cap < need) {
     dfree(c->d_eff);
     c->eff_cap = 0;
     TRY(dalloc(&c->d_eff, need));
     c->eff_cap = need;
   }
+  c->eff_stride = per;
   HIP_TRY(hipMemsetAsync(c->d_eff, 0, need * sizeof(double), c->stream));
   if (!c->d_ones) {
     std::vector<double> ones(nL, 1.0);
@@ -234,7 +249,11 @@ int build_contracted(frei_ctx* c, bool shared_fast) {
   TRY(h2d(c->d_prow, prow.data(), nL, c->stream));
   const double* tabs[kMaxFastS];
   for (int s = 0; s < S; ++s) tabs[s] = c->sp[s].d_tab;
-  launch_contract(tabs, S, c->d_mmr, c->d_prow, nL, q0.n_T, q0.stride, c->d_eff, c->stream);
+  if (batch)  // K7: [n_atm x S] . [S x n_T*pitch] per layer on fp64 MFMA
+    launch_contract_batch(tabs, S, c->d_mmr, c->d_prow, nL, q0.n_T, q0.stride, c->n_atm,
+                          (int64_t)per, c->d_eff, c->stream);
+  else
+    launch_contract(tabs, S, c->d_mmr, c->d_prow, nL, q0.n_T, q0.stride, c->d_eff, c->stream);
   HIP_TRY(hipGetLastError());
   SpecMeta m = c->smeta[0];
   m.tab = c->d_eff;
@@ -335,13 +354,15 @@ int build_meta(frei_ctx* c) {
   TRY(h2d(c->d_pmeta, c->pmeta.data(), (size_t)S * nL, c->stream));
   TRY(h2d(c->d_tnodes, c->tnodes.data(), c->tnodes.size(), c->stream));
   TRY(h2d(c->d_tperm, c->tperm.data(), c->tperm.size(), c->stream));
-  if (c->mmr.size() != (size_t)S * nL) return fail("frei_set_mmr must be called");
-  TRY(h2d(c->d_mmr, c->mmr.data(), (size_t)S * nL, c->stream));
+  if (c->mmr.size() != (size_t)S * nL * c->n_atm) return fail("frei_set_mmr must be called");
+  TRY(h2d(c->d_mmr, c->mmr.data(), (size_t)S * nL * c->n_atm, c->stream));
   TRY(build_contracted(c, fast && shared));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->meta_dirty = false;
   return 0;
 }
+
+AtmStride atm_stride(frei_ctx* c);
 
 SetupArgs setup_args(frei_ctx* c) {
   SetupArgs u{};
@@ -363,6 +384,7 @@ SetupArgs setup_args(frei_ctx* c) {
   u.fsteps = c->d_fsteps;
   u.ssteps = c->d_ssteps;
   u.shared = c->shared;
+  u.bs = atm_stride(c);
   return u;
 }
 
@@ -441,6 +463,8 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     f.dtaus = o.dtaus;
     f.part = c->d_part;
     f.conv = c->d_conv;
+    f.bs = atm_stride(c);
+    f.n_atm = c->n_atm;
     // Prefetch depth: below ~2 waves per SIMD (small per-GPU slices, e.g. 500k lambda over
     // 8 GPUs) a second layer in flight hides HBM latency; at full occupancy one suffices.
     // With one table (K3) and few blocks per CU, four steps in flight add the
@@ -449,7 +473,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
                       : (S_run == 1 && c->nblocks <= c->depth4_max_blocks) ? 4 : 2;
     bool nan_check = false;
     for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
-    if (c->eff && c->shared && c->nblocks <= c->pair_max_blocks) {
+    if (c->eff && c->shared && (int64_t)c->nblocks * c->n_atm <= c->pair_max_blocks) {
       nb_run = (int)((c->nlam + kBlock / 2 - 1) / (kBlock / 2));
       launch_sweep_pair(o.dir, f, nb_run, c->stream);
     } else {
@@ -461,7 +485,11 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   }
   HIP_TRY(hipGetLastError());
   if (c->timing) HIP_TRY(hipEventRecord(e1, c->stream));
-  launch_reduce(c->d_part, nb_run, c->d_Fb, ns * 4, c->d_conv, o.force, c->stream);
+  {
+    const AtmStride bs = atm_stride(c);
+    launch_reduce(c->d_part, nb_run, c->d_Fb, ns * 4, c->d_conv, o.force, c->stream,
+                  c->n_atm, bs.part, bs.fb);
+  }
   HIP_TRY(hipGetLastError());
   const double* Fb = c->d_Fb;
   if (c->nranks > 1 && c->host_ag) {
@@ -513,26 +541,43 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   u.meta_in_lds = (S_meta * c->nL * (sizeof(PMeta) + sizeof(double)) +
                    S_meta * sizeof(SpecMeta) + (size_t)12 * c->nL * sizeof(double) +
                    c->tnodes.size() * sizeof(double)) <= 64 * 1024;
-  launch_update(u, c->stream);
+  launch_update(u, c->stream, c->n_atm);
   HIP_TRY(hipGetLastError());
   return 0;
 }
 
 int reset_loop_state(frei_ctx* c) {
-  HIP_TRY(hipMemsetAsync(c->d_conv, 0, sizeof(int), c->stream));
-  HIP_TRY(hipMemsetAsync(c->d_iter, 0, sizeof(int), c->stream));
-  HIP_TRY(hipMemsetAsync(c->d_flips, 0, sizeof(int32_t) * c->nL, c->stream));
-  HIP_TRY(hipMemsetAsync(c->d_prev, 0, sizeof(int32_t) * c->nL, c->stream));
-  HIP_TRY(hipMemsetAsync(c->d_ndiff, 0, sizeof(int32_t) * c->nL, c->stream));
+  const size_t A = c->n_atm;
+  HIP_TRY(hipMemsetAsync(c->d_conv, 0, sizeof(int) * A, c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_iter, 0, sizeof(int) * A, c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_flips, 0, sizeof(int32_t) * c->nL * A, c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_prev, 0, sizeof(int32_t) * c->nL * A, c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_ndiff, 0, sizeof(int32_t) * c->nL * A, c->stream));
   return 0;
 }
 
 int ensure_hist(frei_ctx* c, int cap) {
   if (cap <= c->hist_cap) return 0;
   dfree(c->d_hist);
-  TRY(dalloc(&c->d_hist, (size_t)cap * 2 * c->nL));
+  TRY(dalloc(&c->d_hist, (size_t)cap * 2 * c->nL * c->n_atm));
   c->hist_cap = cap;
   return 0;
+}
+
+// Per-atmosphere strides of a batched context (all zero for one atmosphere).
+AtmStride atm_stride(frei_ctx* c) {
+  AtmStride b{};
+  if (c->n_atm <= 1) return b;
+  const int64_t nL = c->nL, ns = nL - 1;
+  b.layers = nL;
+  b.steps = ns;
+  b.fb = ns * 4;
+  b.hist = (int64_t)c->hist_cap * 2 * nL;
+  b.flux = nL * c->nlam;
+  b.tab = (int64_t)c->eff_stride;
+  b.part = ns * 4 * (int64_t)(2 * c->nblocks);
+  b.g = c->d_g;
+  return b;
 }
 
 int ensure_dtaus(frei_ctx* c) {
@@ -559,9 +604,11 @@ int frei_device_count(int* n) {
   return 0;
 }
 
-int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int n_species) {
+static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int n_species,
+                      int n_atm) {
   if (!out) return fail("null argument");
   *out = nullptr;
+  if (n_atm < 1 || n_atm > 65535) return fail("n_atm must be in [1, 65535]");
   if (n_layers < 4 || n_layers > kMaxLayers)
     return fail("n_layers must be in [4, 1024] (the emit top layer uses p[-3])");
   if (n_lam < 2) return fail("n_lam must be >= 2");
@@ -571,6 +618,7 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
   c->nL = n_layers;
   c->nlam = n_lam;
   c->S = n_species;
+  c->n_atm = n_atm;
   c->sp.resize(n_species);
   c->nblocks = (int)((n_lam + kBlock - 1) / kBlock);
   if (const char* e = getenv("FREI_PREFETCH_DEPTH")) c->prefetch_depth = atoi(e);
@@ -587,22 +635,22 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
   if ((rc = set_device(c))) return bail(rc);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail("hipStreamCreate failed"));
-  const size_t NL = n_layers, NS = n_species, ns = n_layers - 1;
-  const size_t F = NL * (size_t)n_lam;
+  const size_t NL = n_layers, NS = n_species, ns = n_layers - 1, A = n_atm;
+  const size_t F = NL * (size_t)n_lam * A;   // per-atmosphere buffers are n_atm blocks
   if ((rc = dalloc(&c->d_c1, n_lam)) || (rc = dalloc(&c->d_lk, n_lam)) ||
       (rc = dalloc(&c->d_sig, n_lam)) || (rc = dalloc(&c->d_ftoa, n_lam)) ||
       (rc = dalloc(&c->d_wtr, n_lam)) || (rc = dalloc(&c->d_p, NL)) || (rc = dalloc(&c->d_lnp, NL)) ||
       (rc = dalloc(&c->d_Fu, F)) || (rc = dalloc(&c->d_Fd, F)) ||
-      (rc = dalloc(&c->d_T, NL)) || (rc = dalloc(&c->d_dT, NL)) ||
-      (rc = dalloc(&c->d_bol, NL * 4)) || (rc = dalloc(&c->d_mmr, NS * NL)) ||
-      (rc = dalloc(&c->d_steps, ns)) || (rc = dalloc(&c->d_terms, ns * NS)) ||
-      (rc = dalloc(&c->d_fsteps, ns)) || (rc = dalloc(&c->d_ssteps, ns)) ||
-      (rc = dalloc(&c->d_part, ns * 4 * (size_t)(2 * c->nblocks))) ||
-      (rc = dalloc(&c->d_Fb, ns * 4)) || (rc = dalloc(&c->d_Fb_all, ns * 4)) ||
-      (rc = dalloc(&c->d_conv, 1)) || (rc = dalloc(&c->d_iter, 1)) ||
-      (rc = dalloc(&c->d_Tb, NL)) || (rc = dalloc(&c->d_Ta, NL)) ||
-      (rc = dalloc(&c->d_flips, NL)) || (rc = dalloc(&c->d_prev, NL)) ||
-      (rc = dalloc(&c->d_ndiff, NL)))
+      (rc = dalloc(&c->d_T, NL * A)) || (rc = dalloc(&c->d_dT, NL * A)) ||
+      (rc = dalloc(&c->d_bol, NL * 4 * A)) || (rc = dalloc(&c->d_mmr, NS * NL * A)) ||
+      (rc = dalloc(&c->d_steps, ns * A)) || (rc = dalloc(&c->d_terms, ns * NS * A)) ||
+      (rc = dalloc(&c->d_fsteps, ns * A)) || (rc = dalloc(&c->d_ssteps, ns * A)) ||
+      (rc = dalloc(&c->d_part, ns * 4 * (size_t)(2 * c->nblocks) * A)) ||
+      (rc = dalloc(&c->d_Fb, ns * 4 * A)) || (rc = dalloc(&c->d_Fb_all, ns * 4)) ||
+      (rc = dalloc(&c->d_conv, A)) || (rc = dalloc(&c->d_iter, A)) ||
+      (rc = dalloc(&c->d_Tb, NL * A)) || (rc = dalloc(&c->d_Ta, NL * A)) ||
+      (rc = dalloc(&c->d_flips, NL * A)) || (rc = dalloc(&c->d_prev, NL * A)) ||
+      (rc = dalloc(&c->d_ndiff, NL * A)) || (A > 1 && (rc = dalloc(&c->d_g, A))))
     return bail(rc);
   if (hipHostMalloc((void**)&c->h_flag, 2 * sizeof(int)) != hipSuccess)
     return bail(fail("hipHostMalloc failed"));
@@ -611,10 +659,21 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
       return bail(fail("hipEventCreate failed"));
   if (hipMemset(c->d_Fu, 0, F * sizeof(double)) != hipSuccess ||
       hipMemset(c->d_Fd, 0, F * sizeof(double)) != hipSuccess ||
-      hipMemset(c->d_conv, 0, sizeof(int)) != hipSuccess)
+      hipMemset(c->d_conv, 0, sizeof(int) * A) != hipSuccess)
     return bail(fail("hipMemset failed"));
+  if (A > 1 && hipHostMalloc((void**)&c->h_conv, 2 * A * sizeof(int)) != hipSuccess)
+    return bail(fail("hipHostMalloc failed"));
   *out = c;
   return 0;
+}
+
+int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int n_species) {
+  return ctx_create(out, device, n_layers, n_lam, n_species, 1);
+}
+
+int frei_ctx_create_batch(frei_ctx** out, int device, int n_layers, int64_t n_lam,
+                          int n_species, int n_atm) {
+  return ctx_create(out, device, n_layers, n_lam, n_species, n_atm);
 }
 
 int frei_ctx_destroy(frei_ctx* c) {
@@ -640,6 +699,8 @@ int frei_ctx_destroy(frei_ctx* c) {
   for (void* p : vv)
     if (p) (void)hipFree(p);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
+  if (c->h_conv) (void)hipHostFree(c->h_conv);
+  dfree(c->d_g);
   if (c->h_ag) (void)hipHostFree(c->h_ag);
   for (auto e : c->flag_ev)
     if (e) (void)hipEventDestroy(e);
@@ -663,6 +724,10 @@ int frei_set_grid(frei_ctx* c, const double* c1, const double* lk, const double*
   c->p_top2 = c->p[c->nL - 1] * c->p[c->nL - 2] / c->p[c->nL - 3];
   c->g = g;
   c->m_bar = m_bar;
+  if (c->n_atm > 1) {  // default gravity of every atmosphere (frei_set_gravity overrides)
+    std::vector<double> gv(c->n_atm, g);
+    TRY(h2d(c->d_g, gv.data(), gv.size(), c->stream));
+  }
   TRY(h2d(c->d_c1, c1, n, c->stream));
   TRY(h2d(c->d_lk, lk, n, c->stream));
   TRY(h2d(c->d_sig, sigma, n, c->stream));
@@ -800,15 +865,26 @@ int frei_set_table_binned(frei_ctx* c, int s, frei_xsec* x, int mode, const doub
 
 int frei_set_mmr(frei_ctx* c, const double* mmr) {
   if (!c || !mmr) return fail("null argument");
-  c->mmr.assign(mmr, mmr + (size_t)c->S * c->nL);
+  c->mmr.assign(mmr, mmr + (size_t)c->S * c->nL * c->n_atm);
   c->meta_dirty = true;
+  return 0;
+}
+
+int frei_set_gravity(frei_ctx* c, const double* g) {
+  if (!c || !g) return fail("null argument");
+  if (c->n_atm < 2) return fail("frei_set_gravity needs a batched context (frei_set_grid sets g)");
+  for (int m = 0; m < c->n_atm; ++m)
+    if (!(g[m] > 0)) return fail("g must be positive");
+  TRY(set_device(c));
+  TRY(h2d(c->d_g, g, c->n_atm, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
 }
 
 int frei_set_fluxes(frei_ctx* c, const double* up, const double* down) {
   if (!c) return fail("null argument");
   TRY(set_device(c));
-  const size_t F = (size_t)c->nL * c->nlam;
+  const size_t F = (size_t)c->nL * c->nlam * c->n_atm;
   if (up) TRY(h2d(c->d_Fu, up, F, c->stream));
   if (down) TRY(h2d(c->d_Fd, down, F, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -818,7 +894,7 @@ int frei_set_fluxes(frei_ctx* c, const double* up, const double* down) {
 int frei_get_fluxes(frei_ctx* c, double* up, double* down) {
   if (!c) return fail("null argument");
   TRY(set_device(c));
-  const size_t F = (size_t)c->nL * c->nlam;
+  const size_t F = (size_t)c->nL * c->nlam * c->n_atm;
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (up) HIP_TRY(hipMemcpy(up, c->d_Fu, F * sizeof(double), hipMemcpyDeviceToHost));
   if (down) HIP_TRY(hipMemcpy(down, c->d_Fd, F * sizeof(double), hipMemcpyDeviceToHost));
@@ -827,10 +903,11 @@ int frei_get_fluxes(frei_ctx* c, double* up, double* down) {
 
 int frei_set_temperatures(frei_ctx* c, const double* T) {
   if (!c || !T) return fail("null argument");
-  for (int l = 0; l < c->nL; ++l)
+  const size_t n = (size_t)c->nL * c->n_atm;
+  for (size_t l = 0; l < n; ++l)
     if (!(T[l] > 0)) return fail("temperatures must be positive");
   TRY(set_device(c));
-  TRY(h2d(c->d_T, T, c->nL, c->stream));
+  TRY(h2d(c->d_T, T, n, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
 }
@@ -839,12 +916,13 @@ int frei_get_temperatures(frei_ctx* c, double* T) {
   if (!c || !T) return fail("null argument");
   TRY(set_device(c));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  HIP_TRY(hipMemcpy(T, c->d_T, c->nL * sizeof(double), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(T, c->d_T, (size_t)c->nL * c->n_atm * sizeof(double), hipMemcpyDeviceToHost));
   return 0;
 }
 
 int frei_sweep(frei_ctx* c, int direction, double alpha, double* dT, double* bol,
                double* dtaus) {
+  if (c && c->n_atm > 1) return fail("frei_sweep is per atmosphere: use frei_iterate / frei_run_batch");
   if (!ready(c)) return fail("context not ready (frei_set_grid)");
   if (direction != FREI_EMIT && direction != FREI_ABSORB) return fail("bad direction");
   TRY(set_device(c));
@@ -881,12 +959,12 @@ int frei_state_init(frei_ctx* c, const double* T_init) {
   if (!ready(c) || !T_init) return fail("context not ready or null T_init");
   TRY(set_device(c));
   TRY(build_meta(c));
-  TRY(frei_set_temperatures(c, T_init));
-  const size_t F = (size_t)c->nL * c->nlam;
+  TRY(h2d(c->d_T, T_init, (size_t)c->nL * c->n_atm, c->stream));
+  const size_t F = (size_t)c->nL * c->nlam * c->n_atm;
   HIP_TRY(hipMemsetAsync(c->d_Fu, 0, F * sizeof(double), c->stream));  // core.py:265-266
   HIP_TRY(hipMemsetAsync(c->d_Fd, 0, F * sizeof(double), c->stream));
   TRY(reset_loop_state(c));
-  launch_setup(setup_args(c), kEmit, c->stream);
+  launch_setup(setup_args(c), kEmit, c->stream, c->n_atm);
   HIP_TRY(hipGetLastError());
   return 0;
 }
@@ -931,6 +1009,7 @@ int frei_run(frei_ctx* c, const double* T_init, int n_timesteps, int n_zero_cros
              double convergence_dT, double alpha, int* n_iter, double* T_final,
              double* temp_hist, double* dtaus, double* spectrum) {
   if (!ready(c) || !T_init || !n_iter) return fail("context not ready or null argument");
+  if (c->n_atm > 1) return fail("batched context: use frei_run_batch");
   if (n_timesteps < 1) return fail("n_timesteps must be >= 1");
   TRY(set_device(c));
   TRY(ensure_hist(c, n_timesteps));
@@ -981,8 +1060,56 @@ int frei_run(frei_ctx* c, const double* T_init, int n_timesteps, int n_zero_cros
   return 0;
 }
 
+int frei_run_batch(frei_ctx* c, const double* T_init, int n_timesteps, int n_zero_crossings,
+                   double convergence_dT, double alpha, int* n_iter, double* T_final,
+                   double* spectra) {
+  if (!ready(c) || !T_init || !n_iter) return fail("context not ready or null argument");
+  if (n_timesteps < 1) return fail("n_timesteps must be >= 1");
+  TRY(set_device(c));
+  TRY(ensure_hist(c, n_timesteps));
+  TRY(frei_state_init(c, T_init));
+  const int A = c->n_atm;
+  int* flags = c->h_conv ? c->h_conv : c->h_flag;   // pinned [2][A]
+  // every atmosphere iterates until its own convergence test holds (its kernels then
+  // return at once); the host polls all flags one chunk behind
+  const int chunk = 4;
+  int launched = 0, k = 0;
+  while (launched < n_timesteps) {
+    const int n = std::min(chunk, n_timesteps - launched);
+    TRY(iterate(c, n, n_zero_crossings, convergence_dT, alpha, true));
+    launched += n;
+    HIP_TRY(hipMemcpyAsync(flags + (k & 1) * A, c->d_conv, A * sizeof(int),
+                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipEventRecord(c->flag_ev[k & 1], c->stream));
+    if (k > 0) {
+      HIP_TRY(hipEventSynchronize(c->flag_ev[(k - 1) & 1]));
+      bool all = true;
+      for (int m = 0; m < A; ++m) all = all && flags[((k - 1) & 1) * A + m] != 0;
+      if (all) break;
+    }
+    ++k;
+  }
+  // final emit of every atmosphere without alpha (alpha = 1, core.py:323-333)
+  SweepOpts f;
+  f.dir = kEmit;
+  f.force = 1;
+  f.alpha = 1.0;
+  TRY(run_sweep(c, f));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(n_iter, c->d_iter, A * sizeof(int), hipMemcpyDeviceToHost));
+  const size_t nL = c->nL;
+  if (T_final)
+    HIP_TRY(hipMemcpy(T_final, c->d_T, nL * A * sizeof(double), hipMemcpyDeviceToHost));
+  if (spectra)  // F_up[n_layers - 1] of every atmosphere
+    HIP_TRY(hipMemcpy2D(spectra, c->nlam * sizeof(double),
+                        c->d_Fu + (nL - 1) * c->nlam, nL * c->nlam * sizeof(double),
+                        c->nlam * sizeof(double), A, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int frei_kappa(frei_ctx* c, double T, double p, double* k, double* sigma) {
   if (!ready(c) || !k) return fail("context not ready or null argument");
+  if (c->n_atm > 1) return fail("frei_kappa is per atmosphere: use a single-atmosphere context");
   TRY(set_device(c));
   TRY(build_meta(c));
   std::vector<TermP> terms(c->S);
@@ -1068,6 +1195,8 @@ int frei_comm_unique_id(void* id128) {
 }
 
 int frei_comm_init(frei_ctx* c, int nranks, int rank, const void* id128) {
+  if (c && c->n_atm > 1)
+    return fail("batched contexts shard atmospheres across ranks: no exchange");
   if (!c || !id128) return fail("null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail("bad rank/nranks");
   TRY(set_device(c));
@@ -1094,6 +1223,8 @@ int frei_comm_init(frei_ctx* c, int nranks, int rank, const void* id128) {
 }
 
 int frei_comm_init_host(frei_ctx* c, int nranks, int rank, frei_allgather_fn fn, void* user) {
+  if (c && c->n_atm > 1)
+    return fail("batched contexts shard atmospheres across ranks: no exchange");
   if (!c || !fn) return fail("null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail("bad rank/nranks");
   TRY(set_device(c));
@@ -1114,6 +1245,7 @@ int frei_comm_init_host(frei_ctx* c, int nranks, int rank, frei_allgather_fn fn,
 // dtaus for post-processing: the caller's host array (uploaded) or the device copy.
 static int post_dtaus(frei_ctx* c, const double* h, double** tmp, const double** d) {
   *tmp = nullptr;
+  if (c->n_atm > 1) return fail("post-processing is per atmosphere: use a single context");
   if (h) {
     const size_t n = (size_t)c->nL * c->nlam;
     TRY(dalloc(tmp, n));

@@ -50,6 +50,25 @@ int frei_device_count(int* n);
 
 /* Context for n_layers x n_lam (local slice) x n_species on `device`. */
 int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int n_species);
+/*
+ * Batched context (§8(f) #2, grid sweeps such as C5): n_atm independent atmospheres share the
+ * wavelength and pressure grids and the opacity tables; each has its own temperatures,
+ * gravity (frei_set_gravity) and mixing ratios (frei_set_mmr takes [n_atm][n_species]
+ * [n_layers]).  The reference has no batch API: each atmosphere is the reference's
+ * Grid.emission_spectrum (core.py:233-338) run independently.  Needs tables on shared
+ * on-node p/T nodes without NaN; the per-atmosphere species contraction runs on fp64 MFMA
+ * (K7).  State accessors (set/get fluxes and temperatures) take n_atm blocks; frei_sweep,
+ * frei_run, frei_kappa, post-processing and the rank exchange are single-atmosphere only
+ * (batched runs shard atmospheres across ranks with no exchange).
+ */
+int frei_ctx_create_batch(frei_ctx** out, int device, int n_layers, int64_t n_lam,
+                          int n_species, int n_atm);
+int frei_set_gravity(frei_ctx* ctx, const double* g);
+/* Every atmosphere iterates to its own convergence (core.py:273-318), then the final emit;
+ * n_iter[n_atm], T_final[n_atm][n_layers] and spectra[n_atm][n_lam] (F_up[n_layers-1]). */
+int frei_run_batch(frei_ctx* ctx, const double* T_init, int n_timesteps, int n_zero_crossings,
+                   double convergence_dT, double alpha, int* n_iter, double* T_final,
+                   double* spectra);
 int frei_ctx_destroy(frei_ctx* ctx);
 
 /*

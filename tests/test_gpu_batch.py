@@ -1,0 +1,119 @@
+"""GPU parity of the batched engine (§8(f) #2, config C5): n_atm atmospheres that differ in
+T, gravity and metallicity, on shared wavelengths, pressures and tables, as one device run
+(sweeps over (wavelength block, atmosphere), per-atmosphere species contraction on fp64
+MFMA).  Each atmosphere is checked against the oracle's emission_spectrum (the reference's
+per-Grid loop) under the flux criterion of tests/parity.py, with identical iteration counts
+to convergence, and against the single-atmosphere engine."""
+import numpy as np
+import pytest
+
+from oracle import frei_oracle as O
+from tests.parity import EPS, assert_flux_parity, rel, row_normwise
+
+pytestmark = pytest.mark.gpu
+
+M_BAR = 4.0142926168559996e-24
+
+
+@pytest.fixture(scope="module")
+def fa():
+    import frei_amd
+    from frei_amd import _native as N
+    assert N.device_count() >= 1, "no HIP device visible"
+    return frei_amd
+
+
+def _setup(fa, n_atm, n_lam, n_layers, names, seed):
+    rng = np.random.default_rng(seed)
+    lam, _, _ = O.wavelength_grid(0.5, 10, n_lam)
+    p = O.pressure_grid(n_layers, -6, np.log10(200))
+    Tn = np.linspace(400.0, 4000.0, 12)
+    tabs_o, tabs_f = {}, {}
+    for n in names:
+        base = 10 ** rng.uniform(-3, 1.5, lam.size)
+        fp, fT = (p / 1.0) ** 0.1, (Tn / 1000.0) ** 0.5
+        tabs_o[n] = O.Table(O.separable_table(base, fp, fT), p, Tn)
+        tabs_f[n] = fa.SeparableTable(base, fp, fT, p, Tn)
+    T_ref = rng.uniform(1100, 2500, n_atm)
+    g = rng.uniform(800.0, 6000.0, n_atm)
+    mh = rng.uniform(-0.5, 1.0, n_atm)
+    mmr0 = O.mock_mmr(names, M_BAR)
+    mmr = np.array([(mmr0 * 10 ** m)[:, None] * np.ones(n_layers) for m in mh])
+    T0 = np.array([O.temperature_grid(p, t, 0.1, 0.1) for t in T_ref])
+    return lam, p, tabs_o, tabs_f, g, mmr, T0
+
+
+def test_batched_atmospheres_match_oracle_per_atmosphere(fa):
+    names = ["1H2-16O", "12C-16O", "Na"]
+    lam, p, tabs_o, tabs_f, g, mmr, T0 = _setup(fa, 5, 2048, 30, names, 17)
+    Ft = O.F_TOA(lam)
+    eng = fa.BatchEngine(lam, p, tabs_f, g=g, mmr=mmr, F_toa=Ft)
+    try:
+        assert eng.path()["contracted"]
+        out = eng.run(T0, n_timesteps=40, n_zero_crossings=2, convergence_dT=3.0, alpha=1.0)
+    finally:
+        eng.close()
+    for m in range(5):
+        cond = dict(up=np.zeros((30, lam.size)), down=np.zeros((30, lam.size)), delta=1.0)
+        osp, oT, oth, odt, ou, od, it = O.emission_spectrum(
+            tabs_o, T0[m], p, lam, Ft, g[m], M_BAR, 1, n_timesteps=40, n_zero_crossings=2,
+            convergence_dT=3.0, mmr=mmr[m], err=cond)
+        assert out["n_iter"][m] == it, f"atmosphere {m}: iterations"
+        relT = rel(out["final_T"][m], oT)
+        assert relT < 1e-10, f"atmosphere {m}: T {relT:.3e}"
+        assert_flux_parity(out["spectra"][m], osp, cond["up"][-1], max(EPS, relT),
+                           f"atmosphere {m} spectrum")
+
+
+def test_batched_mfma_contraction_tiles_and_padding(fa):
+    """17 atmospheres (two 16-row MFMA tiles, one padded) x 5 species (a padded K step):
+    fixed-work iterations agree with one single-atmosphere engine per atmosphere."""
+    names = ["1H2-16O", "12C-16O", "12C-16O2", "Na", "K"]
+    lam, p, tabs_o, tabs_f, g, mmr, T0 = _setup(fa, 17, 700, 16, names, 23)
+    eng = fa.BatchEngine(lam, p, tabs_f, g=g, mmr=mmr)
+    try:
+        eng.state_init(T0)
+        eng.iterate(3)
+        eng.synchronize()
+        up, down = eng.get_fluxes()
+        import ctypes
+        from frei_amd import _native as N
+        Tb = np.empty((17, 16))
+        N.check(N.lib().frei_get_temperatures(eng._ctx, N.dptr(Tb)))
+    finally:
+        eng.close()
+    for m in (0, 7, 16):
+        single = fa.Engine(lam, p, tabs_f, g=g[m], mmr=mmr[m])
+        try:
+            single.state_init(T0[m])
+            single.iterate(3)
+            single.synchronize()
+            su, sd = single.get_fluxes()
+            Ts = single.get_temperatures()
+        finally:
+            single.close()
+        assert rel(Tb[m], Ts) < 1e-12, f"atmosphere {m}: T"
+        assert rel(up[m][-1], su[-1]) < 1e-9, f"atmosphere {m}: emergent F_up"
+
+
+def test_batched_emission_spectra_over_grids(fa):
+    """batched_emission_spectra over Grid objects (a T_ref x g sweep) equals each Grid's own
+    emission_spectrum within the parity tolerance, with the same iteration counts."""
+    lam, _, _ = O.wavelength_grid(0.5, 10, 1024)
+    grids = []
+    op = None
+    for T_ref, g in [(1400, 1500.0), (2000, 2478.6519476149147), (2400, 4000.0)]:
+        pl = fa.Planet.from_hot_jupiter()
+        pl.g = g
+        gr = fa.Grid(pl, lam=lam, n_layers=20, T_ref=T_ref)
+        if op is None:
+            op = fa.load_example_opacity(gr, scale_factor=2)
+        gr.load_opacities(opacities=op)
+        grids.append(gr)
+    res = fa.batched_emission_spectra(grids, n_timesteps=30)
+    for gr, (spec, T, it) in zip(grids, res):
+        s1, T1, th1, _ = gr.emission_spectrum(n_timesteps=30)
+        gr._close_engine()
+        assert it == th1.shape[1] // 2
+        assert rel(T, T1) < 1e-10
+        assert row_normwise(spec.flux, s1.flux) < 1e-9
