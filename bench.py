@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--no-binning", action="store_true",
                     help="skip the K6 opacity-binning measurement (rank 0)")
     ap.add_argument("--binning-reps", type=int, default=5)
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the batched-atmosphere (C5) measurement")
+    ap.add_argument("--c5-lam", type=int, default=100_000)
+    ap.add_argument("--c5-steps", type=int, default=5)
     return ap.parse_args()
 
 
@@ -154,6 +158,66 @@ def binning_leg(a, device, cpu=True):
     return out
 
 
+def c5_leg(a, d):
+    """Config C5 on this rank: 32 atmospheres (T_ref 1000..2400 K step 200 x log g 2.5..4,
+    [M/H] of this rank's slot of 8) x 60 layers x 100k lambda x 8 species, as one batched
+    context (256 atmospheres over 8 GPUs = 32 per GPU, weak scaling, no
+    exchange).  Fixed-work T-P iterations (updates/s) and the run of every atmosphere to its
+    own radiative equilibrium."""
+    from frei_amd.batch import BatchEngine
+    from frei_amd.opacity import SeparableTable
+    from frei_amd.tp import temperature_grid
+    from frei_amd.workloads import c3
+    w = c3(n_layers=a.n_layers, n_lam=a.c5_lam, n_T=16)
+    T_refs = np.arange(1000.0, 2401.0, 200.0)
+    loggs = np.array([2.5, 3.0, 3.5, 4.0])
+    mh = np.linspace(-1.0, 1.0, 8)[d.rank % 8]
+    T0 = np.array([temperature_grid(w["p"], t, 0.1, 0.1) for t in T_refs for _ in loggs])
+    g = np.array([10.0 ** lg for _ in T_refs for lg in loggs])
+    T_nodes = np.linspace(0.8 * T0.min(), 1.2 * T0.max(), 16)
+    fT = (T_nodes / 1000.0) ** 0.5
+    tabs = {n: SeparableTable(w["base"][s], w["fp"][s], fT, w["p"], T_nodes)
+            for s, n in enumerate(w["names"])}
+    mmr = np.broadcast_to(w["mmr"] * 10.0 ** mh, (len(g),) + w["mmr"].shape)
+    A = len(g)
+    t_s = time.perf_counter()
+    eng = BatchEngine(w["lam"], w["p"], tabs, g=g, mmr=mmr, device=d.local)
+    try:
+        eng.state_init(T0)       # metadata + K7 contraction (fp64 MFMA), once
+        eng.synchronize()
+        setup_s = time.perf_counter() - t_s
+        eng.iterate(1)
+        eng.synchronize()
+        d.barrier()
+        t0 = time.perf_counter()
+        eng.iterate(a.c5_steps)
+        eng.synchronize()
+        t1 = time.perf_counter()
+        d.barrier()
+        el = d.max(t1 - t0)
+        upd = 2 * (a.n_layers - 1) * a.c5_lam * A * a.c5_steps * d.world
+        eng.run(T0, n_timesteps=a.rad_eq_max, n_zero_crossings=2, convergence_dT=3.0)
+        d.barrier()
+        t2 = time.perf_counter()
+        out = eng.run(T0, n_timesteps=a.rad_eq_max, n_zero_crossings=2, convergence_dT=3.0)
+        t3 = time.perf_counter()
+        d.barrier()
+        rad = d.max(t3 - t2)
+    finally:
+        eng.close()
+    return {"workload": f"C5: {A} atmospheres per GPU (T_ref 1000..2400 K x log g 2.5..4, "
+                        f"[M/H] {mh:+.2f} on rank 0) x {a.n_layers} layers x {a.c5_lam} "
+                        f"lambda x {len(w['names'])} species, batched, {d.world} GPU(s)",
+            "updates_per_s": upd / el, "ms_per_step": el / a.c5_steps * 1e3,
+            "atmospheres": A * d.world,
+            "rad_eq": {"wall_s": rad, "atmospheres_per_s": A * d.world / rad,
+                       "iterations_min": int(out["n_iter"].min()),
+                       "iterations_max": int(out["n_iter"].max()),
+                       "max_iterations": a.rad_eq_max},
+            "setup_s": setup_s,
+            "note": "setup_s: table generation + metadata + K7 MFMA contraction, once"}
+
+
 def main():
     a = parse()
     d = Dist(a.gpus)
@@ -249,6 +313,7 @@ def main():
                          f"{min(a.cpu_lam, n_lam)} lambda (evenly strided sample of the same "
                          f"grid), {S} species, 1 T-P iteration + final emit, {dt:.1f} s"}
     eng.close()
+    c5 = None if a.no_c5 else c5_leg(a, d)
     binning = None
     if d.rank == 0 and not a.no_binning:
         binning = binning_leg(a, d.local, cpu=(d.world == 1 and not a.no_cpu_baseline))
@@ -294,6 +359,7 @@ def main():
                          "avg_launch_ms": avg_sweep_s * 1e3, "launches": n_sweeps},
             "cpu_baseline": cpu,
             "k6_binning": binning,
+            "c5_batched": c5,
         }
         print(json.dumps(line), flush=True)
 

@@ -3,7 +3,7 @@
 set -e
 mkdir -p gpurun_out/final
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-B="python3 bench.py --steps 10 --warmup 1 --rad-eq-max 1 --no-cpu-baseline --no-binning"
+B="python3 bench.py --steps 10 --warmup 1 --rad-eq-max 1 --no-cpu-baseline --no-binning --no-c5"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/final/pmc_fetch -o run -- $B > gpurun_out/final/pmc_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/final/pmc_write -o run -- $B > gpurun_out/final/pmc_write.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/final/pmc_sq -o run -- $B > gpurun_out/final/pmc_sq.log 2>&1
@@ -14,5 +14,5 @@ timeout -k 10 400 python3 bench.py > gpurun_out/final/bench.json 2> gpurun_out/f
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/final/prof -o run -- python3 bench.py --no-cpu-baseline > gpurun_out/final/bench_under_rocprof.json 2> gpurun_out/final/bench_under_rocprof.err
 # per-GPU slice sizes of the 2/4/8-GPU runs on one GPU (sweep + fixed per-sweep costs)
 for n in 250000 125000 62500; do
-  timeout -k 10 120 python3 bench.py --n-lam $n --steps 20 --no-binning --no-cpu-baseline > gpurun_out/final/bench_n$n.json 2>/dev/null
+  timeout -k 10 120 python3 bench.py --n-lam $n --steps 20 --no-binning --no-cpu-baseline --no-c5 > gpurun_out/final/bench_n$n.json 2>/dev/null
 done
