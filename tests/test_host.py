@@ -1,0 +1,98 @@
+"""Host-side logic that needs no GPU: cross-section file readers, binned_opacity's species
+selection, the batched API's argument checks, and the benchmark's byte accounting (which
+must select the same source rows as the binning plan the oracle pins)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import frei_oracle as O
+
+
+def _xsec_arrays():
+    wl = np.linspace(0.5, 10.0, 40)
+    T = np.array([1000.0, 2000.0])
+    p = np.array([1e-3, 1.0, 10.0])
+    op = np.arange(2 * 3 * 40, dtype=np.float32).reshape(2, 3, 40)
+    return op, T, p, wl
+
+
+def test_open_cross_section_npz_and_netcdf3(tmp_path):
+    import frei_amd as fa
+    op, T, p, wl = _xsec_arrays()
+    path = tmp_path / "1H2-16O_test.npz"
+    np.savez(path, opacity=op, temperature=T, pressure=p, wavelength=wl)
+    x = fa.open_cross_section(str(path))
+    assert x.isotopologue == "1H2-16O" and x.opacity.dtype == np.float32
+    assert np.array_equal(x.opacity, op) and np.array_equal(x.wavelength, wl)
+    from scipy.io import netcdf_file
+    nc = tmp_path / "12C-16O_test.nc"
+    with netcdf_file(str(nc), "w") as f:
+        f.createDimension("temperature", 2)
+        f.createDimension("pressure", 3)
+        f.createDimension("wavelength", 40)
+        for name, dims, arr in (("temperature", ("temperature",), T),
+                                ("pressure", ("pressure",), p),
+                                ("wavelength", ("wavelength",), wl),
+                                ("opacity", ("temperature", "pressure", "wavelength"), op)):
+            v = f.createVariable(name, arr.dtype, dims)
+            v[:] = arr
+    y = fa.open_cross_section(str(nc))
+    assert y.isotopologue == "12C-16O"
+    assert np.array_equal(y.opacity, op) and np.array_equal(y.pressure, p)
+    hdf = tmp_path / "1H2-16O_hdf.nc"
+    hdf.write_bytes(b"\x89HDF\r\n\x1a\n" + b"\0" * 16)
+    with pytest.raises(ValueError, match="netCDF4/HDF5"):
+        fa.open_cross_section(str(hdf))
+
+
+def test_binned_opacity_selects_species_from_files(tmp_path):
+    import frei_amd as fa
+    op, T, p, wl = _xsec_arrays()
+    for iso in ("1H2-16O", "12C-16O", "Na"):
+        np.savez(tmp_path / f"{iso}_x.npz", opacity=op, temperature=T, pressure=p,
+                 wavelength=wl)
+    lam, wl_bins, _ = O.wavelength_grid(0.6, 9.0, 10)
+    T_t, p_t = np.array([1500.0, 1800.0]), np.array([5.0, 0.1])
+    tabs = fa.binned_opacity(T_t, p_t, wl_bins, lam, species=["H2O", "Na"],
+                             path=str(tmp_path / "*.nc"))
+    assert sorted(tabs) == ["1H2-16O", "Na"]
+    t = tabs["Na"]
+    assert t.shape == (2, 2, 10) and t.groupies and np.array_equal(t.pressure, p_t)
+    with pytest.raises(FileNotFoundError):
+        fa.binned_opacity(T_t, p_t, wl_bins, lam, path=str(tmp_path / "none_*.nc"))
+
+
+def test_batched_grids_must_share_grids_and_tables():
+    import frei_amd as fa
+    pl = fa.Planet.from_hot_jupiter()
+    a = fa.Grid(pl, n_wl_bins=64, n_layers=8)
+    b = fa.Grid(pl, n_wl_bins=65, n_layers=8)
+    a.load_opacities(opacities=fa.load_example_opacity(a))
+    b.load_opacities(opacities=a.opacities)
+    with pytest.raises(ValueError, match="wavelengths and pressures"):
+        fa.batched_emission_spectra([a, b])
+    c = fa.Grid(pl, n_wl_bins=64, n_layers=8)
+    c.load_opacities(opacities=fa.load_example_opacity(c))
+    with pytest.raises(ValueError, match="one opacity dict"):
+        fa.batched_emission_spectra([a, c])
+
+
+def test_binning_accounting_selects_the_oracle_rows():
+    from frei_amd.workloads import binning_bytes, binning_workload, nearest_index
+    w = binning_workload(n_layers=12, n_lam=2000, spacing_cm=2.0, n_T_src=7, n_p_src=5)
+    assert np.array_equal(nearest_index(w["T_src"], w["T0"]), O.nearest_index(w["T_src"], w["T0"]))
+    assert np.array_equal(nearest_index(w["p_src"], w["p"]), O.nearest_index(w["p_src"], w["p"]))
+    acc = binning_bytes(w)
+    start, end = O.bin_ranges(w["wl_hi"], w["wl_bins"])
+    assert acc["points"] == int(end[-1] - start[0])
+    rows = {(t, q) for t in O.nearest_index(w["T_src"], w["T0"])
+            for q in O.nearest_index(w["p_src"], w["p"])}
+    assert acc["source_rows"] == len(rows) and acc["dest_rows"] == 144
+
+
+def test_build_script_lists_every_hip_source():
+    from frei_amd import build
+    here = os.path.join(os.path.dirname(build.__file__), "csrc")
+    hips = sorted(f for f in os.listdir(here) if f.endswith(".hip"))
+    assert sorted(os.path.basename(s) for s in build.SOURCES) == hips
