@@ -252,9 +252,9 @@ struct UpdateArgs {
 void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st);
 void launch_sweep_fast(int dir, int S, int depth, bool nan_check, bool shared,
                        const FastArgs& a, int nblocks, hipStream_t st);
-// Paired-lane sweep (two lanes per wavelength, 128 wavelengths per block): contracted
-// single table, step table in LDS; for slices with about one wave per SIMD.
-void launch_sweep_pair(int dir, const FastArgs& a, int nblocks, hipStream_t st);
+// Grouped-lane sweep (Q = 2 or 4 lanes per wavelength, 256/Q wavelengths per block):
+// contracted single table, step table in LDS; for slices with about one wave per SIMD.
+void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStream_t st);
 void launch_nan_scan(const double* x, int64_t n, int* flag, hipStream_t st);
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
                    int force, hipStream_t st, int n_atm = 1, int64_t part_stride = 0,

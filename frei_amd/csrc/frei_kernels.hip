@@ -534,18 +534,18 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   }
 }
 
-// ---------------------------------------------------------------- K1, paired-lane form
+// ---------------------------------------------------------------- K1, grouped-lane form
 // Small slices (e.g. 62.5k lambda per GPU over 8 GPUs) leave about one wave per SIMD, and a
-// lone wave issues a vector instruction only every other slot.  This form spends two lanes
-// per wavelength so the same slice runs twice the waves: lane pair (2m, 2m+1) owns
-// wavelength m of the wave's 32, and within each group of two sweep steps the even lane
-// computes step k's coefficients and the odd lane step k+1's (one instruction stream for
-// both).  The carried recurrence then runs through the pair in order (carry broadcast by
-// DPP), each lane stores its own step, and the bolometric terms of the two steps are
-// reduced together over the 32 lanes of each parity (5 exchanges for 8 sums).  Fluxes are
-// formed by the same expressions in the same order as the one-lane form (bit-identical);
-// the bolometric partial sums use this form's own fixed summation tree.  One contracted
-// table (K3), step table staged in LDS.
+// lone wave issues a vector instruction only every other slot.  This form spends Q = 2 or 4
+// lanes per wavelength so the same slice runs Q times the waves: the Q lanes (q = lane mod Q)
+// of a wavelength own its steps Qg + q, so within each group of Q sweep steps every lane
+// computes one step's coefficients (one instruction stream for all Q).  Each lane forms its
+// step's new Planck value and the group resolves (B1, B2) of all Q steps in order; the
+// carried recurrence runs through the group's lanes in step order (carry broadcast by DPP
+// quad_perm); each lane stores its own step; the bolometric terms of the Q steps reduce
+// together over the 64/Q lanes of each q.  Fluxes are formed by the same expressions in the
+// same order as the one-lane form (bit-identical); the bolometric partial sums use this
+// form's own fixed summation tree.  One contracted table (K3), step table staged in LDS.
 template <int CTRL>
 __device__ __forceinline__ double dpp_bcast(double x) {
   const int2 v = __builtin_bit_cast(int2, x);
@@ -554,30 +554,38 @@ __device__ __forceinline__ double dpp_bcast(double x) {
   r.y = __builtin_amdgcn_mov_dpp(v.y, CTRL, 0xF, 0xF, false);
   return __builtin_bit_cast(double, r);
 }
-constexpr int kQpEven = 0xA0;  // quad_perm [0,0,2,2]: each pair reads its even lane
-constexpr int kQpOdd = 0xF5;   // quad_perm [1,1,3,3]: each pair reads its odd lane
-constexpr int kQpSwap = 0xB1;  // quad_perm [1,0,3,2]: partner lane
+// quad_perm control reading sub-lane R of a lane's Q-group (Q = 2: two groups per quad)
+template <int Q, int R>
+constexpr int qp_from() {
+  return Q == 4 ? R * 0x55 : (R | (R << 2) | ((R + 2) << 4) | ((R + 2) << 6));
+}
+template <int Q, int R>
+__device__ __forceinline__ double from_lane(double x) {
+  return dpp_bcast<qp_from<Q, R>()>(x);
+}
 
-// Sums of q0..q3 over the 32 lanes of each parity (lane bit 0).  Lane h + 2b + 4c ends
-// with the sum of q[2b + c] over the lanes of parity h.  Fixed order: deterministic.
-__device__ __forceinline__ double pair_sum4(double q0, double q1, double q2, double q3,
-                                            int lane) {
-  const bool b = lane & 2;
-  const double r0 = __shfl_xor(b ? q0 : q2, 2, 64);
-  const double r1 = __shfl_xor(b ? q1 : q3, 2, 64);
+// Sums of q0..q3 over the 64/Q lanes with the same lane mod Q.  Lane q + Q(b + 2c) ends with
+// the sum of q[2b + c] over the lanes of its residue q.  Fixed order: deterministic.
+template <int Q>
+__device__ __forceinline__ double group_sum4(double q0, double q1, double q2, double q3,
+                                             int lane) {
+  const bool b = lane & Q;
+  const double r0 = __shfl_xor(b ? q0 : q2, Q, 64);
+  const double r1 = __shfl_xor(b ? q1 : q3, Q, 64);
   const double x0 = (b ? q2 : q0) + r0;
   const double x1 = (b ? q3 : q1) + r1;
-  const bool c = lane & 4;
-  double y = (c ? x1 : x0) + __shfl_xor(c ? x0 : x1, 4, 64);
+  const bool c = lane & (2 * Q);
+  double y = (c ? x1 : x0) + __shfl_xor(c ? x0 : x1, 2 * Q, 64);
 #pragma unroll
-  for (int o = 8; o <= 32; o <<= 1) y += __shfl_xor(y, o, 64);
+  for (int o = 4 * Q; o <= 32; o <<= 1) y += __shfl_xor(y, o, 64);
   return y;
 }
 
-template <int DIR>
-__global__ __launch_bounds__(kBlock) void sweep_pair_kernel(
+template <int DIR, int Q>
+__global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     FastArgs a, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
     double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
+  static_assert(Q == 2 || Q == 4, "2 or 4 lanes per wavelength");
   {  // atmosphere of a batched launch (identity for one atmosphere)
     const int m = blockIdx.y;
     Fu += m * a.bs.flux;
@@ -593,9 +601,9 @@ __global__ __launch_bounds__(kBlock) void sweep_pair_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
-  const int h = lane & 1;          // step parity this lane computes
+  const int q = lane & (Q - 1);    // step residue this lane computes
   const int64_t nl = a.n_lam;
-  const int64_t j0 = (int64_t)blockIdx.x * (kBlock / 2) + wv * 32 + (lane >> 1);
+  const int64_t j0 = (int64_t)blockIdx.x * (kBlock / Q) + wv * (64 / Q) + lane / Q;
   const bool act = j0 < nl;
   const int64_t j = act ? j0 : nl - 1;
   const double c1 = a.c1[j], lk = a.lk[j], sig = a.sig[j];
@@ -611,9 +619,9 @@ __global__ __launch_bounds__(kBlock) void sweep_pair_kernel(
   }
   const FastStepS* sp = reinterpret_cast<const FastStepS*>(lss);
   auto clampk = [&](int k) { return k < ns ? k : ns - 1; };
-  // loads of this lane's step in group g (step 2g + h, clamped for a dummy step)
+  // loads of this lane's step in group g (step Qg + q, clamped for a dummy step)
   auto load = [&](int g, double& vlo, double& vhi, double& stale) {
-    const int k = clampk(2 * g + h);
+    const int k = clampk(Q * g + q);
     const double* r = tab + sp[k].off + j;
     vlo = stream_load(r);
     vhi = stream_load(r + a.pitch);
@@ -633,14 +641,14 @@ __global__ __launch_bounds__(kBlock) void sweep_pair_kernel(
       carryB = planck(c1, lk, sp[0].T2);
     }
   }
-  // Phase A of this lane's step in group g (opacity, dtau, albedo, Planck chain of the
-  // pair); refills the group's buffer with group g + 2.
-  struct PairA {
+  struct GroupA {
     double w0, dtau, B1, B2, F_st;
     int k;
   };
-  auto phaseA = [&](int g, double& vlo, double& vhi, double& stale, PairA& A) {
-    const int k = 2 * g + h;
+  // Phase A of this lane's step in group g (opacity, dtau, albedo, Planck chain of the
+  // group); refills the group's buffer with group g + 2.
+  auto phaseA = [&](int g, double& vlo, double& vhi, double& stale, GroupA& A) {
+    const int k = Q * g + q;
     const FastStepS& st = sp[clampk(k)];
     A.k = k;
     A.F_st = stale;
@@ -648,46 +656,66 @@ __global__ __launch_bounds__(kBlock) void sweep_pair_kernel(
     load(g + 2, vlo, vhi, stale);
     A.dtau = st.dm * kap;
     A.w0 = sig / (sig + kap);
-    // each lane forms its step's new Planck value; the pair exchanges them and both lanes
-    // resolve (B1, B2) of both steps in order (emit: B2 is new and becomes the next B1;
-    // absorb: B1 is new and becomes the next B2)
+    // each lane forms its step's new Planck value; the group gathers them and resolves
+    // (B1, B2) of its steps in order (emit: B2 is new and becomes the next B1; absorb: B1 is
+    // new and becomes the next B2; emit's top step keeps B2 = B1)
     const double X = planck(c1, lk, DIR == kEmit ? st.T2 : st.T1);
-    const double Xo = dpp_bcast<kQpSwap>(X);
-    const double X0 = h ? Xo : X, X1 = h ? X : Xo;
-    const bool top0 = sp[clampk(2 * g)].top, top1 = sp[clampk(2 * g + 1)].top;
-    const double Bn0 = (DIR == kEmit && top0) ? carryB : X0;
-    const double Bn1 = (DIR == kEmit && top1) ? Bn0 : X1;
+    double Xr[Q], Bn[Q];
+    Xr[0] = from_lane<Q, 0>(X);
+    Xr[1] = from_lane<Q, 1>(X);
+    if constexpr (Q == 4) {
+      Xr[2] = from_lane<Q, 2>(X);
+      Xr[3] = from_lane<Q, 3>(X);
+    }
+    double prev = carryB;
+#pragma unroll
+    for (int r = 0; r < Q; ++r) {
+      const bool top = sp[clampk(Q * g + r)].top;
+      Bn[r] = (DIR == kEmit && top) ? prev : Xr[r];
+      prev = Bn[r];
+    }
+    double before = carryB, mine = Bn[0];
+#pragma unroll
+    for (int r = 1; r < Q; ++r) {
+      before = (q == r) ? Bn[r - 1] : before;
+      mine = (q == r) ? Bn[r] : mine;
+    }
     if (DIR == kEmit) {
-      A.B1 = h ? Bn0 : carryB;
-      A.B2 = h ? Bn1 : Bn0;
+      A.B1 = before;
+      A.B2 = mine;
     } else {
-      A.B2 = h ? Bn0 : carryB;
-      A.B1 = h ? X1 : X0;
+      A.B2 = before;
+      A.B1 = mine;
     }
-    carryB = Bn1;
+    carryB = Bn[Q - 1];
   };
-  // Carried recurrence through the pair (the even lane's step, then the odd lane's),
-  // stores of this lane's step and the reduction of the pair's bolometric terms.
-  auto finish = [&](const PairA& A, const StepCoef& c) {
+  // Carried recurrence through the group (steps in order), stores of this lane's step and
+  // the reduction of the group's bolometric terms.
+  auto finish = [&](const GroupA& A, const StepCoef& c) {
     const double F_st = A.F_st;
-    const double mid0 = carry;
-    double F2u_a, F1d_a, F2u_b, F1d_b;
-    {
+    auto recur = [&](double in, double& F2u, double& F1d) {
       double F1u, F2d;
-      if (DIR == kEmit) { F1u = mid0; F2d = F_st; } else { F2d = mid0; F1u = F_st; }
-      F2u_a = c.ic * ((c.psi * F1u - c.xi * F2d) + c.Xu);
-      F1d_a = c.ic * ((c.psi * F2d - c.xi * F1u) + c.Xd);
+      if (DIR == kEmit) { F1u = in; F2d = F_st; } else { F2d = in; F1u = F_st; }
+      F2u = c.ic * ((c.psi * F1u - c.xi * F2d) + c.Xu);
+      F1d = c.ic * ((c.psi * F2d - c.xi * F1u) + c.Xd);
+    };
+    double cin = carry, F2u = 0.0, F1d = 0.0, in_r = carry;
+#pragma unroll
+    for (int r = 0; r < Q; ++r) {
+      double a2u, a1d;
+      recur(in_r, a2u, a1d);            // meaningful in lane q == r
+      if (q == r) {
+        cin = in_r;
+        F2u = a2u;
+        F1d = a1d;
+      }
+      const double out = (DIR == kEmit) ? a2u : a1d;
+      if (r == 0) in_r = from_lane<Q, 0>(out);
+      else if (r == 1) in_r = from_lane<Q, 1>(out);
+      else if (r == 2) in_r = from_lane<Q, (Q == 4 ? 2 : 0)>(out);
+      else in_r = from_lane<Q, (Q == 4 ? 3 : 0)>(out);
     }
-    const double mid = dpp_bcast<kQpEven>(DIR == kEmit ? F2u_a : F1d_a);
-    {
-      double F1u, F2d;
-      if (DIR == kEmit) { F1u = mid; F2d = F_st; } else { F2d = mid; F1u = F_st; }
-      F2u_b = c.ic * ((c.psi * F1u - c.xi * F2d) + c.Xu);
-      F1d_b = c.ic * ((c.psi * F2d - c.xi * F1u) + c.Xd);
-    }
-    carry = dpp_bcast<kQpOdd>(DIR == kEmit ? F2u_b : F1d_b);
-    const double cin = h ? mid : mid0;
-    const double F2u = h ? F2u_b : F2u_a, F1d = h ? F1d_b : F1d_a;
+    carry = in_r;
     const double F1u = (DIR == kEmit) ? cin : F_st;
     const double F2d = (DIR == kEmit) ? F_st : cin;
     const int k = A.k;
@@ -700,17 +728,17 @@ __global__ __launch_bounds__(kBlock) void sweep_pair_kernel(
       if (st_dn) Fd[(int64_t)i * nl + j] = F1d;
       if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = c.dtau;
     }
-    const double y = pair_sum4(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
-    const int kq = (k - h) + (lane & 1);
-    if (lane < 8 && kq < ns)
-      red[((int64_t)wv * ns + kq) * 4 + ((lane >> 1) & 1) * 2 + ((lane >> 2) & 1)] = y;
+    const double y = group_sum4<Q>(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
+    const int kq = (k - q) + (lane & (Q - 1));
+    if (lane < 4 * Q && kq < ns)
+      red[((int64_t)wv * ns + kq) * 4 + ((lane / Q) & 1) * 2 + ((lane / (2 * Q)) & 1)] = y;
   };
-  const int ng = (ns + 1) / 2;
-  double la, ha, sa, lb, hb, sb;   // two groups (four steps) in flight
+  const int ng = (ns + Q - 1) / Q;
+  double la, ha, sa, lb, hb, sb;   // two groups in flight
   load(0, la, ha, sa);
   load(1, lb, hb, sb);
   for (int g = 0; g < ng; g += 2) {
-    PairA A0, A1;
+    GroupA A0, A1;
     phaseA(g, la, ha, sa, A0);
     phaseA(g + 1, lb, hb, sb, A1);   // a dummy group past the end is computed, not stored
     StepCoef c0, c1;
@@ -733,18 +761,28 @@ __global__ __launch_bounds__(kBlock) void sweep_pair_kernel(
   }
 }
 
-void launch_sweep_pair(int dir, const FastArgs& a, int nblocks, hipStream_t st) {
+// Q lanes per wavelength: kBlock / Q wavelengths per block.
+void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStream_t st) {
   const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double) +
                      (size_t)a.n_steps * sizeof(FastStepS);
-  if (dir == kEmit)
-    hipLaunchKernelGGL(sweep_pair_kernel<kEmit>, dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1),
-                       dim3(kBlock), shm, st, a,
-                       a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
-  else
-    hipLaunchKernelGGL(sweep_pair_kernel<kAbsorb>, dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1),
-                       dim3(kBlock), shm, st, a,
-                       a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+  const dim3 grid(nblocks, a.n_atm > 1 ? a.n_atm : 1);
+  if (Q == 4) {
+    if (dir == kEmit)
+      hipLaunchKernelGGL((sweep_group_kernel<kEmit, 4>), grid, dim3(kBlock), shm, st, a,
+                         a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+    else
+      hipLaunchKernelGGL((sweep_group_kernel<kAbsorb, 4>), grid, dim3(kBlock), shm, st, a,
+                         a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+  } else {
+    if (dir == kEmit)
+      hipLaunchKernelGGL((sweep_group_kernel<kEmit, 2>), grid, dim3(kBlock), shm, st, a,
+                         a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+    else
+      hipLaunchKernelGGL((sweep_group_kernel<kAbsorb, 2>), grid, dim3(kBlock), shm, st, a,
+                         a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+  }
 }
+
 
 // ---------------------------------------------------------------- partial sums
 __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ part,

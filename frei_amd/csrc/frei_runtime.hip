@@ -163,7 +163,9 @@ struct frei_ctx {
   int shared_max_blocks = 1024;
   // Paired-lane sweep (two lanes per wavelength): contracted table, LDS step table and at
   // most this many 256-wavelength blocks, i.e. about one wave per SIMD or less.
-  int pair_max_blocks = 1024;           // FREI_PAIR_MAX_BLOCKS (<= 262k lambda per GPU)
+  int pair_max_blocks = 640;            // FREI_PAIR_MAX_BLOCKS (<= 164k lambda per GPU)
+  int quad_max_blocks = 128;            // FREI_QUAD_MAX_BLOCKS (<= 32k lambda per GPU)
+  int group_q = 0;                      // FREI_GROUP_Q forces 1, 2 or 4 lanes per wavelength
   int depth4_max_blocks = 0;            // FREI_DEPTH4_MAX_BLOCKS (4 steps in flight: off, measured no faster)
   frei_allgather_fn host_ag = nullptr;  // host all-gather callback (alternative to RCCL)
   void* host_ag_user = nullptr;
@@ -364,6 +366,17 @@ int build_meta(frei_ctx* c) {
 
 AtmStride atm_stride(frei_ctx* c);
 
+// Lanes per wavelength of the sweep: the grouped-lane kernel (2 or 4 lanes) when the slice
+// leaves about one wave per SIMD or less (contracted table, LDS step table), else 1.
+int group_lanes(frei_ctx* c) {
+  if (!(c->fast && c->eff && c->shared)) return 1;
+  if (c->group_q > 0) return c->group_q;
+  const int64_t blocks = (int64_t)c->nblocks * c->n_atm;   // 256-wavelength blocks
+  if (blocks <= c->quad_max_blocks) return 4;
+  if (blocks <= c->pair_max_blocks) return 2;
+  return 1;
+}
+
 SetupArgs setup_args(frei_ctx* c) {
   SetupArgs u{};
   u.n_layers = c->nL;
@@ -473,9 +486,10 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
                       : (S_run == 1 && c->nblocks <= c->depth4_max_blocks) ? 4 : 2;
     bool nan_check = false;
     for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
-    if (c->eff && c->shared && (int64_t)c->nblocks * c->n_atm <= c->pair_max_blocks) {
-      nb_run = (int)((c->nlam + kBlock / 2 - 1) / (kBlock / 2));
-      launch_sweep_pair(o.dir, f, nb_run, c->stream);
+    const int Q = group_lanes(c);
+    if (Q > 1) {
+      nb_run = (int)((c->nlam + kBlock / Q - 1) / (kBlock / Q));
+      launch_sweep_group(o.dir, Q, f, nb_run, c->stream);
     } else {
       launch_sweep_fast(o.dir, S_run, depth, nan_check && !c->eff, c->shared != 0, f,
                         c->nblocks, c->stream);
@@ -575,7 +589,7 @@ AtmStride atm_stride(frei_ctx* c) {
   b.hist = (int64_t)c->hist_cap * 2 * nL;
   b.flux = nL * c->nlam;
   b.tab = (int64_t)c->eff_stride;
-  b.part = ns * 4 * (int64_t)(2 * c->nblocks);
+  b.part = ns * 4 * (int64_t)(4 * c->nblocks);
   b.g = c->d_g;
   return b;
 }
@@ -627,6 +641,11 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
   if (const char* e = getenv("FREI_PRECONTRACT")) c->eff_mode = atoi(e) ? 1 : 0;
   if (const char* e = getenv("FREI_DEPTH4_MAX_BLOCKS")) c->depth4_max_blocks = atoi(e);
   if (const char* e = getenv("FREI_PAIR_MAX_BLOCKS")) c->pair_max_blocks = atoi(e);
+  if (const char* e = getenv("FREI_QUAD_MAX_BLOCKS")) c->quad_max_blocks = atoi(e);
+  if (const char* e = getenv("FREI_GROUP_Q")) {
+    const int q = atoi(e);
+    c->group_q = (q == 1 || q == 2 || q == 4) ? q : 0;
+  }
   auto bail = [&](int rc) {
     frei_ctx_destroy(c);
     return rc;
@@ -645,7 +664,7 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
       (rc = dalloc(&c->d_bol, NL * 4 * A)) || (rc = dalloc(&c->d_mmr, NS * NL * A)) ||
       (rc = dalloc(&c->d_steps, ns * A)) || (rc = dalloc(&c->d_terms, ns * NS * A)) ||
       (rc = dalloc(&c->d_fsteps, ns * A)) || (rc = dalloc(&c->d_ssteps, ns * A)) ||
-      (rc = dalloc(&c->d_part, ns * 4 * (size_t)(2 * c->nblocks) * A)) ||
+      (rc = dalloc(&c->d_part, ns * 4 * (size_t)(4 * c->nblocks) * A)) ||
       (rc = dalloc(&c->d_Fb, ns * 4 * A)) || (rc = dalloc(&c->d_Fb_all, ns * 4)) ||
       (rc = dalloc(&c->d_conv, A)) || (rc = dalloc(&c->d_iter, A)) ||
       (rc = dalloc(&c->d_Tb, NL * A)) || (rc = dalloc(&c->d_Ta, NL * A)) ||
@@ -1313,9 +1332,9 @@ int frei_ctx_path(frei_ctx* c, int* flags) {
   TRY(build_meta(c));
   int nan = 0;
   for (const auto& q : c->sp) nan = nan || q.has_nan;
-  const bool pair = c->fast && c->eff && c->shared && c->nblocks <= c->pair_max_blocks;
+  const int Q = group_lanes(c);
   *flags = (c->fast ? 1 : 0) | (c->fast && c->shared ? 2 : 0) | (c->eff ? 4 : 0) |
-           (nan ? 8 : 0) | (pair ? 16 : 0);
+           (nan ? 8 : 0) | (Q == 2 ? 16 : 0) | (Q == 4 ? 32 : 0);
   return 0;
 }
 

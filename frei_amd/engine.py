@@ -264,7 +264,7 @@ class Engine:
         N.check(N.lib().frei_ctx_path(self._ctx, ctypes.byref(f)))
         v = f.value
         return dict(fast=bool(v & 1), lds_steps=bool(v & 2), contracted=bool(v & 4),
-                    nan=bool(v & 8), paired=bool(v & 16))
+                    nan=bool(v & 8), paired=bool(v & 16), quad=bool(v & 32))
 
     def kappa(self, T, p_bar):
         k = np.empty(self.n_lam)

@@ -185,8 +185,8 @@ int frei_contribution(frei_ctx* ctx, const double* dtaus, const double* nu,
 /* Which sweep implementation the context's current tables select (after metadata build):
  * bit 0 fast path (on-node pressures, >= 2 T nodes, S <= 8), bit 1 step table staged in
  * LDS (shared brackets, small slices), bit 2 species-contracted table (K3), bit 3 tables
- * hold NaN (per-species nansum variant), bit 4 paired-lane sweep (two lanes per
- * wavelength, small slices). */
+ * hold NaN (per-species nansum variant), bit 4 / bit 5 grouped-lane sweep with two / four
+ * lanes per wavelength (small slices). */
 int frei_ctx_path(frei_ctx* ctx, int* flags);
 
 /* Timing of the sweep kernel (HIP events on the context stream around every sweep

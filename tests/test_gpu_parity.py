@@ -328,42 +328,46 @@ def test_species_contraction_matches_per_species_sum(fa, monkeypatch):
         assert_flux_parity(down, od, cond["down"], delta, "F_down " + mode)
 
 
-def test_paired_lane_sweep_matches_one_lane_form(fa, monkeypatch):
-    """The paired-lane sweep (two lanes per wavelength, small slices) forms every flux with
-    the one-lane expressions: one sweep from the same state gives bit-identical fluxes and
-    dtaus; only the bolometric partial sums use another fixed summation tree (dT within
-    1e-10), so T-P iterations agree within the parity tolerance."""
+@pytest.mark.parametrize("n_layers", [34, 36])     # 33 / 35 steps: dummy group slots
+def test_grouped_lane_sweep_matches_one_lane_form(fa, monkeypatch, n_layers):
+    """The grouped-lane sweeps (two or four lanes per wavelength, small slices) form every
+    flux with the one-lane expressions: one sweep from the same state gives bit-identical
+    fluxes and dtaus; only the bolometric partial sums use another fixed summation tree (dT
+    within 1e-10), so T-P iterations agree within the parity tolerance."""
     rng = np.random.default_rng(9)
     lam, _, _ = O.wavelength_grid(0.5, 10, 5000)
-    p = O.pressure_grid(33, -6, np.log10(200))        # odd step count: a dummy pair slot
+    p = O.pressure_grid(n_layers, -6, np.log10(200))
     T0 = O.temperature_grid(p, 1600.0, 0.1, 0.1)
     Tn = np.linspace(0.8 * T0.min(), 1.2 * T0.max(), 9)
     names = ["1H2-16O", "12C-16O", "Na"]
     tabs = {n: fa.SeparableTable(10 ** rng.uniform(-4, 2, lam.size), (p / 1.0) ** 0.1,
                                  (Tn / 1000.0) ** 0.5, p, Tn) for n in names}
-    mmr = O.mock_mmr(names, M_BAR)[:, None] * np.ones(33)
+    mmr = O.mock_mmr(names, M_BAR)[:, None] * np.ones(n_layers)
     out = {}
-    for mode in ("pair", "one"):
-        monkeypatch.setenv("FREI_PAIR_MAX_BLOCKS", "512" if mode == "pair" else "0")
+    for q in (4, 2, 1):
+        monkeypatch.setenv("FREI_GROUP_Q", str(q))
         eng = fa.Engine(lam, p, tabs, mmr=mmr)
         try:
-            assert eng.path()["paired"] == (mode == "pair")
+            path = eng.path()
+            assert (path["paired"], path["quad"]) == (q == 2, q == 4)
             r = {}
             for d in (0, 1):    # emit then absorb from the same initial state
                 eng.set_temperatures(T0)
-                eng.set_fluxes(np.full((33, lam.size), 1e9), np.full((33, lam.size), 2e8))
+                eng.set_fluxes(np.full((n_layers, lam.size), 1e9),
+                               np.full((n_layers, lam.size), 2e8))
                 r[d] = eng.sweep(d, alpha=1.0) + eng.get_fluxes()
             r["run"] = eng.run(T0, n_timesteps=4, n_zero_crossings=10 ** 6,
                                convergence_dT=-1.0)
-            out[mode] = r
+            out[q] = r
         finally:
             eng.close()
-    for d in (0, 1):
-        dT_p, bol_p, dt_p, up_p, dn_p = out["pair"][d]
-        dT_o, bol_o, dt_o, up_o, dn_o = out["one"][d]
-        assert np.array_equal(up_p, up_o) and np.array_equal(dn_p, dn_o), f"dir {d} fluxes"
-        assert np.array_equal(dt_p, dt_o), f"dir {d} dtaus"
-        assert row_normwise(bol_p, bol_o) < 1e-12
-        assert np.all(np.abs(dT_p - dT_o) <= 1e-10 * np.abs(dT_o) + 1e-300)
-    assert rel(out["pair"]["run"]["final_T"], out["one"]["run"]["final_T"]) < 1e-12
-    assert row_normwise(out["pair"]["run"]["spectrum"], out["one"]["run"]["spectrum"]) < 1e-9
+    for q in (4, 2):
+        for d in (0, 1):
+            dT_p, bol_p, dt_p, up_p, dn_p = out[q][d]
+            dT_o, bol_o, dt_o, up_o, dn_o = out[1][d]
+            assert np.array_equal(up_p, up_o) and np.array_equal(dn_p, dn_o), f"Q{q} dir {d}"
+            assert np.array_equal(dt_p, dt_o), f"Q{q} dir {d} dtaus"
+            assert row_normwise(bol_p, bol_o) < 1e-12
+            assert np.all(np.abs(dT_p - dT_o) <= 1e-10 * np.abs(dT_o) + 1e-300)
+        assert rel(out[q]["run"]["final_T"], out[1]["run"]["final_T"]) < 1e-12
+        assert row_normwise(out[q]["run"]["spectrum"], out[1]["run"]["spectrum"]) < 1e-9

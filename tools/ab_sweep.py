@@ -1,6 +1,8 @@
 """A/B timing of sweep-kernel builds (same C ABI) interleaved in ONE process.
 
-    python tools/ab_sweep.py NAME=path/to/lib.so [NAME=...] [--n-lam N] [--rounds R]
+    python tools/ab_sweep.py NAME=path/to/lib.so[:Q] [NAME=...] [--n-lam N] [--rounds R]
+
+A ":Q" suffix forces Q lanes per wavelength (FREI_GROUP_Q) for that context.
 
 Each library gets its own context on device 0 with the C3 workload; rounds alternate
 between builds (MI355X guide §5.4 rule 24) and report median / min ms per sweep.
@@ -30,6 +32,9 @@ def main():
     builds = []
     for a in args:
         name, path = a.split("=", 1)
+        q = None
+        if ":" in path:
+            path, q = path.rsplit(":", 1)
         N._lib = None
         N.LIB_PATH = os.path.abspath(path)
         lib = N.lib()
@@ -38,7 +43,10 @@ def main():
         from frei_amd.opacity import SeparableTable
         tabs = {n: SeparableTable(w["base"][s], w["fp"][s], w["fT"][s], w["p"], w["T_nodes"])
                 for s, n in enumerate(names)}
+        if q is not None:
+            os.environ["FREI_GROUP_Q"] = q
         eng = E.Engine(w["lam"], w["p"], tabs, mmr=w["mmr"][:S], device=0)
+        os.environ.pop("FREI_GROUP_Q", None)
         eng.state_init(w["T0"])
         eng.iterate(1)
         eng.synchronize()
