@@ -18,6 +18,7 @@
 // expression order, so results differ from NumPy only by the last-ulp differences of
 // exp/expm1/sqrt (ocml vs libm).  See DESIGN.md "Parity".
 #include "frei_device.h"
+#include "frei_math.h"
 
 namespace frei {
 
@@ -27,7 +28,7 @@ __device__ __forceinline__ double planck(double c1, double lk, double T) {
 #ifdef FREI_MEMONLY
   return c1 * lk * T;
 #else
-  return c1 / expm1(kHC / (lk * T));
+  return fm::div_big(c1, fm::expm1(fm::div(kHC, lk * T)));
 #endif
 }
 
@@ -39,21 +40,21 @@ __device__ __forceinline__ void two_stream(double w0, double dtau, double B1, do
   // are exact without the multiply/divide, and sqrt(E * Emw) == sqrt(Emw / E), so that
   // branch skips two divisions and a square root with bit-identical results.
   double E, Emw, sq, r, q;
-  const double Bp = (B1 - B2) / dtau;
+  const double Bp = fm::div(B1 - B2, dtau);
   if (w0 > 0.1) {
     E = (1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0);
     Emw = E - w0;
-    sq = sqrt(E * Emw);
-    r = sqrt(Emw / E);
-    q = Bp / (2.0 * E);
+    sq = fm::sqrt(E * Emw);
+    r = fm::sqrt(fm::div(Emw, E));
+    q = fm::div(Bp, 2.0 * E);
   } else {
     E = 1.0;
     Emw = 1.0 - w0;
-    sq = sqrt(Emw);
+    sq = fm::sqrt(Emw);
     r = sq;
     q = Bp * 0.5;
   }
-  const double Tr = exp((-2.0 * sq) * dtau);
+  const double Tr = fm::exp((-2.0 * sq) * dtau);
   const double zp = 0.5 * (1.0 + r);
   const double zm = 0.5 * (1.0 - r);
   const double Tr2 = Tr * Tr;
@@ -62,8 +63,8 @@ __device__ __forceinline__ void two_stream(double w0, double dtau, double B1, do
   const double chi = zm2 * Tr2 - zp2;
   const double xi = (zp * zm) * (1.0 - Tr2);
   const double psi = (zm2 - zp2) * Tr;
-  const double pi_w = (kPi * (1.0 - w0)) / Emw;
-  const double ic = 1.0 / chi;
+  const double pi_w = fm::div(kPi * (1.0 - w0), Emw);
+  const double ic = fm::div(1.0, chi);
   F2u = ic * ((psi * F1u - xi * F2d) +
               pi_w * ((B2 * (chi + xi) - psi * B1) + q * ((chi - psi) - xi)));
   F1d = ic * ((psi * F2d - xi * F1u) +
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     const int i = sp.layer;
     const double kap = kappa_at<S, FAST>(a.terms + (int64_t)k * nS, nS, j, sig);
     const double dtau = sp.dm * kap;             // twostream.py:227-231
-    const double w0 = sig / (sig + kap);         // twostream.py:376-378
+    const double w0 = fm::div(sig, sig + kap);   // twostream.py:376-378
     double B1, B2, F1u, F2d;
     if (DIR == kEmit) {
       B1 = Bc;
@@ -260,7 +261,7 @@ struct StepCoef {
 __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, double B2,
                                           double Emw, double sq, double r, double q,
                                           StepCoef& c) {
-  const double Tr = exp((-2.0 * sq) * dtau);
+  const double Tr = fm::exp((-2.0 * sq) * dtau);
   const double zp = 0.5 * (1.0 + r);
   const double zm = 0.5 * (1.0 - r);
   const double Tr2 = Tr * Tr;
@@ -269,10 +270,10 @@ __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, dou
   const double chi = zm2 * Tr2 - zp2;
   const double xi = (zp * zm) * (1.0 - Tr2);
   const double psi = (zm2 - zp2) * Tr;
-  const double pi_w = (kPi * (1.0 - w0)) / Emw;
+  const double pi_w = fm::div(kPi * (1.0 - w0), Emw);
   c.psi = psi;
   c.xi = xi;
-  c.ic = 1.0 / chi;
+  c.ic = fm::div(1.0, chi);
   c.Xu = pi_w * ((B2 * (chi + xi) - psi * B1) + q * ((chi - psi) - xi));
   c.Xd = pi_w * ((B1 * (chi + xi) - psi * B2) + q * ((xi + psi) - chi));
   c.dtau = dtau;
@@ -283,8 +284,8 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
                                           StepCoef& c) {
   const double E = (w0 > 0.1) ? ((1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0)) : 1.0;
   const double Emw = E - w0;
-  const double q = ((B1 - B2) / dtau) / (2.0 * E);
-  coef_tail(w0, dtau, B1, B2, Emw, sqrt(E * Emw), sqrt(Emw / E), q, c);
+  const double q = fm::div(fm::div(B1 - B2, dtau), 2.0 * E);
+  coef_tail(w0, dtau, B1, B2, Emw, fm::sqrt(E * Emw), fm::sqrt(fm::div(Emw, E)), q, c);
 }
 
 // Step whose w0 <= 0.1 (E = 1): E * Emw, Emw / E and Bprime / (2 E) are exact without the
@@ -293,8 +294,8 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
 __device__ __forceinline__ void coef_e1(double w0, double dtau, double B1, double B2,
                                         StepCoef& c) {
   const double Emw = 1.0 - w0;
-  const double sq = sqrt(Emw);
-  coef_tail(w0, dtau, B1, B2, Emw, sq, sq, ((B1 - B2) / dtau) * 0.5, c);
+  const double sq = fm::sqrt(Emw);
+  coef_tail(w0, dtau, B1, B2, Emw, sq, sq, fm::div(B1 - B2, dtau) * 0.5, c);
 }
 
 struct PreCoef {
@@ -431,7 +432,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     load(k + PD, v, stale);
     const double kap = tot + sig;
     const double dtau = dm * kap;
-    const double w0 = sig / (sig + kap);
+    const double w0 = fm::div(sig, sig + kap);
     double B1, B2;
     if (DIR == kEmit) {
       B1 = Bprev;
@@ -655,7 +656,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     const double kap = st.mmr[0] * ((0.0 + vlo * st.wlo) + vhi * st.whi) + sig;
     load(g + 2, vlo, vhi, stale);
     A.dtau = st.dm * kap;
-    A.w0 = sig / (sig + kap);
+    A.w0 = fm::div(sig, sig + kap);
     // each lane forms its step's new Planck value; the group gathers them and resolves
     // (B1, B2) of its steps in order (emit: B2 is new and becomes the next B1; absorb: B1 is
     // new and becomes the next B2; emit's top step keeps B2 = B1)

@@ -1,0 +1,149 @@
+// frei_math.h — fp64 exp / expm1 / sqrt / division for the sweep kernels, bit-identical to
+// the ocml / LLVM lowering they replace but cheaper on gfx950's VALU.
+//
+// Why: the sweep is fp64-VALU-bound, and three lowering choices cost ~25% of
+// its instructions per flux update:
+//   * ocml's exp/expm1 Horner chains are emitted as `v_fmac_f64 acc(=c_k) += r * p`, so every
+//     polynomial coefficient is first copied into a VGPR pair (two v_mov_b32 per term, ~18
+//     VALU moves per call).  Here each term is one `v_fma_f64 p, r, p, s[c_k]` with the
+//     coefficient in an SGPR pair (materialised by SALU moves, off the VALU port).
+//   * IEEE fp64 division is lowered with v_div_scale x2 / v_div_fmas / v_div_fixup around the
+//     Newton-Raphson core.  Those only act when an operand is within ~2^768 of the exponent
+//     range ends or denormal; every quotient the sweep forms (optical depths, Planck terms,
+//     albedos, 1/chi) is far from them, so the bare core below returns the same bits.
+//   * sqrt's denormal-range scaling (x < 2^-767) is likewise dropped: the sweep takes square
+//     roots of 1 - w0 style quantities in (2^-53, 2].
+// Every function keeps the exact operation sequence of the lowering it replaces (same
+// constants, same fma order), so results are identical wherever the dropped guards would not
+// fire; tools/mathcheck.hip checks that on the GPU over random and edge-case inputs.
+#pragma once
+#include <hip/hip_runtime.h>
+
+// A/B switches (tools/build_variant.sh -DFREI_FM_...=0|1): 0 selects the plain ocml / IEEE
+// form.  FREI_FM_EXP is off: in the sweep the SGPR-held coefficients push the kernel past
+// the SGPR file (18 spills through v_writelane/v_readlane), which measured 2% slower than the
+// VGPR moves it removes (profiles/r01_ab_fastmath.txt).  Division and sqrt are on (-6%).
+#ifndef FREI_FM_EXP
+#define FREI_FM_EXP 0
+#endif
+#ifndef FREI_FM_DIV
+#define FREI_FM_DIV 1
+#endif
+#ifndef FREI_FM_SQRT
+#define FREI_FM_SQRT 1
+#endif
+
+namespace frei {
+namespace fm {
+
+// d = a * b + c with c held in an SGPR pair (wave-uniform constant).
+__device__ __forceinline__ double fma_sc(double a, double b, double c) {
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+  return d;
+}
+
+__device__ __forceinline__ double c64(unsigned long long bits) {
+  return __builtin_bit_cast(double, bits);
+}
+
+// exp(x): ocml __ocml_exp_f64 (round-to-nearest reduction by ln2 split in two, degree-11
+// Horner polynomial, two final fma with 1.0, ldexp; x > 1024 -> inf, x < -1075 -> 0).
+__device__ __forceinline__ double exp(double x) {
+#if !FREI_FM_EXP
+  return ::exp(x);
+#endif
+  const double n = __builtin_rint(x * c64(0x3ff71547652b82feull));
+  double r = __builtin_fma(c64(0xbfe62e42fefa39efull), n, x);
+  r = __builtin_fma(c64(0xbc7abc9e3b39803full), n, r);
+  double p = __builtin_fma(c64(0x3e5ade156a5dcb37ull), r, c64(0x3e928af3fca7ab0cull));
+  p = fma_sc(r, p, c64(0x3ec71dee623fde64ull));
+  p = fma_sc(r, p, c64(0x3efa01997c89e6b0ull));
+  p = fma_sc(r, p, c64(0x3f2a01a014761f6eull));
+  p = fma_sc(r, p, c64(0x3f56c16c1852b7b0ull));
+  p = fma_sc(r, p, c64(0x3f81111111122322ull));
+  p = fma_sc(r, p, c64(0x3fa55555555502a1ull));
+  p = fma_sc(r, p, c64(0x3fc5555555555511ull));
+  p = fma_sc(r, p, c64(0x3fe000000000000bull));
+  p = __builtin_fma(r, p, 1.0);
+  p = __builtin_fma(r, p, 1.0);
+  double e = __builtin_ldexp(p, (int)n);
+  e = (x > 1024.0) ? __builtin_inf() : e;   // NaN passes through, as in ocml
+  return (x < -1075.0) ? 0.0 : e;
+}
+
+// expm1(x): ocml __ocml_expm1_f64 (same reduction, degree-12 polynomial for e^r - 1 - r,
+// scale 2^n with the n = 1024 split, x > 709.78 -> inf, x < -37 -> -1).
+__device__ __forceinline__ double expm1(double x) {
+#if !FREI_FM_EXP
+  return ::expm1(x);
+#endif
+  const double n = __builtin_rint(x * c64(0x3ff71547652b82feull));
+  double r = __builtin_fma(c64(0xbfe62e42fefa39efull), n, x);
+  r = __builtin_fma(c64(0xbc7abc9e3b39803full), n, r);
+  double p = __builtin_fma(c64(0x3e21f32ea9d67f34ull), r, c64(0x3e5af4eb2a1b768bull));
+  p = fma_sc(r, p, c64(0x3e927e500e0ac05bull));
+  p = fma_sc(r, p, c64(0x3ec71de01b889c29ull));
+  p = fma_sc(r, p, c64(0x3efa01a0197bcfd8ull));
+  p = fma_sc(r, p, c64(0x3f2a01a01ac1a723ull));
+  p = fma_sc(r, p, c64(0x3f56c16c16c18931ull));
+  p = fma_sc(r, p, c64(0x3f81111111110056ull));
+  p = fma_sc(r, p, c64(0x3fa5555555555552ull));
+  p = fma_sc(r, p, c64(0x3fc5555555555557ull));
+  p = r * __builtin_fma(r, p, 0.5);
+  const bool top = (n == 1024.0);
+  const double s = top ? c64(0x7fe0000000000000ull) : __builtin_ldexp(1.0, (int)n);
+  const double t = s - 1.0;
+  const double u = __builtin_fma(r, p, r);
+  double y = __builtin_fma(s, u, t);
+  y = top ? y + y : y;
+  y = (x > c64(0x40862e42fefa39efull)) ? __builtin_inf() : y;
+  return (x < -37.0) ? -1.0 : y;
+}
+
+// a / b: LLVM's fp64 division core (rcp, two Newton-Raphson steps, quotient, one residual
+// correction) without the div_scale / div_fmas / div_fixup range guards.
+__device__ __forceinline__ double div(double a, double b) {
+#if !FREI_FM_DIV
+  return a / b;
+#endif
+  double r = __builtin_amdgcn_rcp(b);
+  double e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double q = a * r;
+  const double rem = __builtin_fma(-b, q, a);
+  return __builtin_fma(rem, r, q);
+}
+
+// c / x for x from expm1 of a Planck exponent: x can exceed 2^900 (x -> inf for very cold
+// layers at short wavelengths), where the unguarded core would lose the denormal quotient;
+// those lanes take the IEEE division (a rarely taken, execz-skipped branch).
+__device__ __forceinline__ double div_big(double a, double b) {
+  double q = div(a, b);
+  if (__builtin_expect(!(b < 0x1p900), 0)) q = a / b;
+  return q;
+}
+
+// sqrt(x): ocml's rsq + Newton-Raphson sequence without the x < 2^-767 rescaling; +-0 and
+// +inf pass through as in ocml.
+__device__ __forceinline__ double sqrt(double x) {
+#if !FREI_FM_SQRT
+  return ::sqrt(x);
+#endif
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y;
+  double h = y * 0.5;
+  const double e = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, e, g);
+  h = __builtin_fma(h, e, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  return __builtin_amdgcn_class(x, 0x260) ? x : g;   // +-0, +inf
+}
+
+}  // namespace fm
+}  // namespace frei
