@@ -109,22 +109,83 @@ __device__ __forceinline__ double kappa_at(const TermP* __restrict__ t, int nS, 
   return tot + sig;  // k includes sigma (Q1)
 }
 
-// Sum four per-lane values over the wave64 with 7 exchanges (instead of 4 x 6): after the
-// first two butterfly levels each lane carries one of the four partial sums.  Lane 0 ends
-// with sum(q0), lane 2 with sum(q1), lane 1 with sum(q2), lane 3 with sum(q3).  Fixed order
-// (commutative pairs), so the result is deterministic.
+// ---------------------------------------------------------------- cross-lane sums
+// DPP move of a double (two 32-bit halves): row_mask / bank_mask all, bound_ctrl off.
+template <int CTRL>
+__device__ __forceinline__ double dpp_bcast(double x) {
+  const int2 v = __builtin_bit_cast(int2, x);
+  int2 r;
+  r.x = __builtin_amdgcn_mov_dpp(v.x, CTRL, 0xF, 0xF, false);
+  r.y = __builtin_amdgcn_mov_dpp(v.y, CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, r);
+}
+
+// Value of lane ^ M for M <= 8, all on the VALU (no LDS round trip): quad_perm for 1 and 2,
+// row_shl / row_shr selected by the lane's bit for 4, row_ror:8 (= xor 8) for 8.
+template <int M>
+__device__ __forceinline__ double lane_xor(double x, int lane) {
+  static_assert(M == 1 || M == 2 || M == 4 || M == 8, "in-row exchange");
+  if constexpr (M == 1) return dpp_bcast<0xB1>(x);            // quad_perm [1,0,3,2]
+  if constexpr (M == 2) return dpp_bcast<0x4E>(x);            // quad_perm [2,3,0,1]
+  if constexpr (M == 4) {
+    // both moves on the full wave, then the select: a DPP inside a divergent branch would
+    // read its partner lane while that lane is masked off
+    const double down = dpp_bcast<0x114>(x);   // row_shr:4 (lane - 4)
+    const double up = dpp_bcast<0x104>(x);     // row_shl:4 (lane + 4)
+    return (lane & 4) ? down : up;
+  }
+  return dpp_bcast<0x128>(x);                                 // row_ror:8
+}
+
+// x(row r) + x(row r ^ 1) and x(half h) + x(half h ^ 1) through gfx950's
+// v_permlane16_swap / v_permlane32_swap: both operands hold x, the swap leaves the even
+// rows (halves) in one result and the odd ones in the other, so every lane adds the same
+// two values in the same order.
+__device__ __forceinline__ double rows_sum16(double x) {
+  const int2 v = __builtin_bit_cast(int2, x);
+  const auto lo = __builtin_amdgcn_permlane16_swap(v.x, v.x, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(v.y, v.y, false, false);
+  return __builtin_bit_cast(double, make_int2((int)lo[0], (int)hi[0])) +
+         __builtin_bit_cast(double, make_int2((int)lo[1], (int)hi[1]));
+}
+__device__ __forceinline__ double rows_sum32(double x) {
+  const int2 v = __builtin_bit_cast(int2, x);
+  const auto lo = __builtin_amdgcn_permlane32_swap(v.x, v.x, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(v.y, v.y, false, false);
+  return __builtin_bit_cast(double, make_int2((int)lo[0], (int)hi[0])) +
+         __builtin_bit_cast(double, make_int2((int)lo[1], (int)hi[1]));
+}
+
+// Sums of q0..q3 over the 64/Q lanes with the same lane mod Q (Q = 1: the whole wave).
+// The first two butterfly levels exchange one of two values each, so afterwards every lane
+// carries one partial sum: lane q + Q(b + 2c) ends with the sum of q[2b + c] over the lanes
+// of its residue q.  Every level is a DPP or permlane-swap VALU operation (the shfl form
+// costs one LDS round trip per level, which a one- or two-wave-per-SIMD slice cannot hide).
+// Fixed tree: deterministic.
+template <int Q>
+__device__ __forceinline__ double group_sum4(double q0, double q1, double q2, double q3,
+                                             int lane) {
+  const bool b = lane & Q;
+  const double r0 = lane_xor<Q>(b ? q0 : q2, lane);
+  const double r1 = lane_xor<Q>(b ? q1 : q3, lane);
+  const double x0 = (b ? q2 : q0) + r0;
+  const double x1 = (b ? q3 : q1) + r1;
+  const bool c = lane & (2 * Q);
+  double y = (c ? x1 : x0) + lane_xor<2 * Q>(c ? x0 : x1, lane);
+  if constexpr (Q == 1) {
+    y += dpp_bcast<0x124>(y);   // row_ror:4 then row_ror:8: the 4 lanes of a residue mod 4
+    y += dpp_bcast<0x128>(y);
+  } else if constexpr (Q == 2) {
+    y += dpp_bcast<0x128>(y);   // row_ror:8 (lane ^ 8)
+  }
+  return rows_sum32(rows_sum16(y));
+}
+
+// One-lane form: lane 0 ends with sum(q0), lane 2 with sum(q1), lane 1 with sum(q2), lane 3
+// with sum(q3).
 __device__ __forceinline__ double wave_sum4(double q0, double q1, double q2, double q3,
                                             int lane) {
-  const bool odd = lane & 1;
-  const double r0 = __shfl_xor(odd ? q0 : q2, 1, 64);
-  const double r1 = __shfl_xor(odd ? q1 : q3, 1, 64);
-  const double x0 = (odd ? q2 : q0) + r0;
-  const double x1 = (odd ? q3 : q1) + r1;
-  const bool b1 = lane & 2;
-  double y = (b1 ? x1 : x0) + __shfl_xor(b1 ? x0 : x1, 2, 64);
-#pragma unroll
-  for (int o = 4; o <= 32; o <<= 1) y += __shfl_xor(y, o, 64);
-  return y;
+  return group_sum4<1>(q0, q1, q2, q3, lane);
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -249,6 +310,19 @@ __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlan
 __device__ __forceinline__ int64_t uni(int64_t x) {
   return (int64_t)__double_as_longlong(uni(__longlong_as_double((long long)x)));
 }
+
+// Step parameters that only feed arithmetic (T1, T2, dm, weights, mmr): with
+// FREI_UNI_VGPR they are read from the LDS step table straight into VGPRs (uniform values, a
+// broadcast LDS read) instead of readfirstlane'd into SGPRs: two VALU readfirstlanes fewer
+// per double, and no SGPR pressure from the steps in flight.
+#ifndef FREI_UNI_VGPR
+#define FREI_UNI_VGPR 1
+#endif
+#if FREI_UNI_VGPR
+#define UNIV(x) (x)
+#else
+#define UNIV(x) uni(x)
+#endif
 
 struct StepCoef {
   double psi, xi, ic, Xu, Xd;  // F2u = ic*((psi*F1u - xi*F2d) + Xu), F1d likewise with Xd
@@ -398,9 +472,9 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     if constexpr (SH) {
       c.layer = uni(sp[kk].layer);
       c.top = uni(sp[kk].top);
-      T1 = uni(sp[kk].T1);
-      T2 = uni(sp[kk].T2);
-      dm = uni(sp[kk].dm);
+      T1 = UNIV(sp[kk].T1);
+      T2 = UNIV(sp[kk].T2);
+      dm = UNIV(sp[kk].dm);
     } else {
       c.layer = st[kk].layer;
       c.top = st[kk].top;
@@ -420,7 +494,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
 #endif
       double ops;
       if constexpr (SH) {
-        ops = uni(sp[kk].mmr[s]) * ((0.0 + vlo * uni(sp[kk].wlo)) + vhi * uni(sp[kk].whi));
+        ops = UNIV(sp[kk].mmr[s]) * ((0.0 + vlo * UNIV(sp[kk].wlo)) + vhi * UNIV(sp[kk].whi));
       } else {
         ops = st[kk].mmr[s] * ((0.0 + vlo * st[kk].wlo[s]) + vhi * st[kk].whi[s]);
       }
@@ -547,14 +621,6 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
 // together over the 64/Q lanes of each q.  Fluxes are formed by the same expressions in the
 // same order as the one-lane form (bit-identical); the bolometric partial sums use this
 // form's own fixed summation tree.  One contracted table (K3), step table staged in LDS.
-template <int CTRL>
-__device__ __forceinline__ double dpp_bcast(double x) {
-  const int2 v = __builtin_bit_cast(int2, x);
-  int2 r;
-  r.x = __builtin_amdgcn_mov_dpp(v.x, CTRL, 0xF, 0xF, false);
-  r.y = __builtin_amdgcn_mov_dpp(v.y, CTRL, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, r);
-}
 // quad_perm control reading sub-lane R of a lane's Q-group (Q = 2: two groups per quad)
 template <int Q, int R>
 constexpr int qp_from() {
@@ -565,22 +631,6 @@ __device__ __forceinline__ double from_lane(double x) {
   return dpp_bcast<qp_from<Q, R>()>(x);
 }
 
-// Sums of q0..q3 over the 64/Q lanes with the same lane mod Q.  Lane q + Q(b + 2c) ends with
-// the sum of q[2b + c] over the lanes of its residue q.  Fixed order: deterministic.
-template <int Q>
-__device__ __forceinline__ double group_sum4(double q0, double q1, double q2, double q3,
-                                             int lane) {
-  const bool b = lane & Q;
-  const double r0 = __shfl_xor(b ? q0 : q2, Q, 64);
-  const double r1 = __shfl_xor(b ? q1 : q3, Q, 64);
-  const double x0 = (b ? q2 : q0) + r0;
-  const double x1 = (b ? q3 : q1) + r1;
-  const bool c = lane & (2 * Q);
-  double y = (c ? x1 : x0) + __shfl_xor(c ? x0 : x1, 2 * Q, 64);
-#pragma unroll
-  for (int o = 4 * Q; o <= 32; o <<= 1) y += __shfl_xor(y, o, 64);
-  return y;
-}
 
 template <int DIR, int Q>
 __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
