@@ -26,6 +26,9 @@
 #ifndef FREI_FM_EXP
 #define FREI_FM_EXP 0
 #endif
+#ifndef FREI_FM_EXPM1
+#define FREI_FM_EXPM1 FREI_FM_EXP
+#endif
 #ifndef FREI_FM_DIV
 #define FREI_FM_DIV 1
 #endif
@@ -75,7 +78,7 @@ __device__ __forceinline__ double exp(double x) {
 // expm1(x): ocml __ocml_expm1_f64 (same reduction, degree-12 polynomial for e^r - 1 - r,
 // scale 2^n with the n = 1024 split, x > 709.78 -> inf, x < -37 -> -1).
 __device__ __forceinline__ double expm1(double x) {
-#if !FREI_FM_EXP
+#if !FREI_FM_EXPM1
   return ::expm1(x);
 #endif
   const double n = __builtin_rint(x * c64(0x3ff71547652b82feull));
