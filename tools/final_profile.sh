@@ -16,3 +16,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 for n in 250000 125000 62500; do
   timeout -k 10 120 python3 bench.py --n-lam $n --steps 20 --no-binning --no-cpu-baseline --no-c5 > gpurun_out/final/bench_n$n.json 2>/dev/null
 done
+# per-sweep timeline (kernel durations and gaps) at the 8-GPU slice size
+timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/final/prof_n62500 -o run -- python3 bench.py --n-lam 62500 --steps 20 --rad-eq-max 1 --no-binning --no-cpu-baseline --no-c5 > gpurun_out/final/bench_n62500_under_rocprof.json 2>/dev/null
+python3 tools/timeline.py gpurun_out/final/prof_n62500/run_kernel_trace.csv > gpurun_out/final/timeline_n62500.txt
+python3 tools/timeline.py gpurun_out/final/prof/run_kernel_trace.csv > gpurun_out/final/timeline_n500000.txt

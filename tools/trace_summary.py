@@ -35,13 +35,21 @@ def main():
     rows = load(sys.argv[1])
     by = {}
     for r in rows:
-        by.setdefault(r["Kernel_Name"], []).append(
+        # launches of one kernel with different grids (e.g. the 500k-lambda headline sweep and
+        # the batched C5 sweep) are separate rows
+        grid = ""
+        if "Grid_Size_X" in r:
+            grid = f"{int(r['Grid_Size_X']) // max(int(r.get('Workgroup_Size_X', 1)), 1)}"
+            if int(r.get("Grid_Size_Y", 1)) > 1:
+                grid += f"x{r['Grid_Size_Y']}"
+        by.setdefault((r["Kernel_Name"], grid), []).append(
             (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    print(f"{'kernel':70s} {'calls':>6s} {'mean_us':>10s} {'median_us':>10s} {'no-op':>6s} {'mean_real_us':>12s}")
-    for name, d in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+    print(f"{'kernel':62s} {'grid':>9s} {'calls':>6s} {'mean_us':>10s} {'median_us':>10s} "
+          f"{'no-op':>6s} {'mean_real_us':>12s}")
+    for (name, grid), d in sorted(by.items(), key=lambda kv: -sum(kv[1])):
         med = st.median(d)
         real = [x for x in d if x > 0.05 * med]
-        print(f"{name[:70]:70s} {len(d):6d} {st.mean(d):10.2f} {med:10.2f} "
+        print(f"{name[:62]:62s} {grid:>9s} {len(d):6d} {st.mean(d):10.2f} {med:10.2f} "
               f"{len(d) - len(real):6d} {st.mean(real):12.2f}")
     if len(sys.argv) > 2:
         b = json.load(open(sys.argv[2]))
