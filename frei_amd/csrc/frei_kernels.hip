@@ -32,6 +32,19 @@ __device__ __forceinline__ double planck(double c1, double lk, double T) {
 #endif
 }
 
+#ifndef FREI_EXPM1_VREG
+#define FREI_EXPM1_VREG 1
+#endif
+// The sweeps' Planck values: expm1 coefficients in VGPRs (fm::Expm1Reg, loaded once).
+__device__ __forceinline__ double planck(double c1, double lk, double T, const fm::Expm1Reg& k) {
+#if FREI_EXPM1_VREG && !defined(FREI_MEMONLY)
+  return fm::div_big(c1, fm::expm1(fm::div(kHC, lk * T), k));
+#else
+  (void)k;
+  return planck(c1, lk, T);
+#endif
+}
+
 // twostream.py:97-177 with g_0 = 0 (call sites 389, 518), E() of :70-94.
 __device__ __forceinline__ void two_stream(double w0, double dtau, double B1, double B2,
                                            double F1u, double F2d, double& F2u,
@@ -405,6 +418,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   const double c1 = a.c1[j], lk = a.lk[j], sig = a.sig[j];
   const double wt = act ? a.wtr[j] : 0.0;
   const int ns = a.n_steps;
+  const fm::Expm1Reg ek = fm::expm1_regs();
   // Shared brackets: stage the whole step table (ns x 120 B) in LDS once, so every step
   // reads its uniform parameters at LDS latency instead of scalar loads that miss the
   // K$ and L2 of a freshly scheduled CU (the step table was written by the update kernel).
@@ -510,11 +524,11 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     double B1, B2;
     if (DIR == kEmit) {
       B1 = Bprev;
-      B2 = c.top ? Bprev : planck(c1, lk, T2);
+      B2 = c.top ? Bprev : planck(c1, lk, T2, ek);
       c.Bnext = B2;
     } else {
       B2 = Bprev;
-      B1 = planck(c1, lk, T1);
+      B1 = planck(c1, lk, T1, ek);
       c.Bnext = B1;
     }
     pc.w0 = w0;
@@ -575,10 +589,10 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     const double T10 = SH ? sp[0].T1 : st[0].T1, T20 = SH ? sp[0].T2 : st[0].T2;
     if (DIR == kEmit) {
       carry = Fu[(int64_t)l0 * nl + j];
-      Bc = planck(c1, lk, T10);
+      Bc = planck(c1, lk, T10, ek);
     } else {
       carry = Fd[(int64_t)(l0 + 1) * nl + j];
-      Bc = planck(c1, lk, T20);
+      Bc = planck(c1, lk, T20, ek);
     }
   }
   // PD steps in flight: their loads are issued PD steps ahead, their coefficients form one
@@ -660,6 +674,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   const double c1 = a.c1[j], lk = a.lk[j], sig = a.sig[j];
   const double wt = act ? a.wtr[j] : 0.0;
   const int ns = a.n_steps;
+  const fm::Expm1Reg ek = fm::expm1_regs();
   const double* __restrict__ tab = a.tab[0];
   double* lss = red + (int64_t)(kBlock / 64) * ns * 4;
   {
@@ -686,10 +701,10 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     const int l0 = sp[0].layer;
     if (DIR == kEmit) {
       carry = Fu[(int64_t)l0 * nl + j];
-      carryB = planck(c1, lk, sp[0].T1);
+      carryB = planck(c1, lk, sp[0].T1, ek);
     } else {
       carry = Fd[(int64_t)(l0 + 1) * nl + j];
-      carryB = planck(c1, lk, sp[0].T2);
+      carryB = planck(c1, lk, sp[0].T2, ek);
     }
   }
   struct GroupA {
@@ -710,7 +725,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     // each lane forms its step's new Planck value; the group gathers them and resolves
     // (B1, B2) of its steps in order (emit: B2 is new and becomes the next B1; absorb: B1 is
     // new and becomes the next B2; emit's top step keeps B2 = B1)
-    const double X = planck(c1, lk, DIR == kEmit ? st.T2 : st.T1);
+    const double X = planck(c1, lk, DIR == kEmit ? st.T2 : st.T1, ek);
     double Xr[Q], Bn[Q];
     Xr[0] = from_lane<Q, 0>(X);
     Xr[1] = from_lane<Q, 1>(X);

@@ -104,6 +104,48 @@ __device__ __forceinline__ double expm1(double x) {
   return (x < -37.0) ? -1.0 : y;
 }
 
+// expm1 with its polynomial coefficients held in VGPRs for a whole kernel: the same
+// operation sequence as fm::expm1 / ocml (bit-identical), but the coefficients are loaded
+// once through an index the compiler cannot prove uniform (mbcnt of an empty mask = 0), so
+// they cannot be rematerialised as literal moves inside the loop (two v_mov_b32 per term per
+// call otherwise; 10 VGPR pairs instead).
+__device__ const double kExpm1Coef[10] = {
+    __builtin_bit_cast(double, 0x3e21f32ea9d67f34ull), __builtin_bit_cast(double, 0x3e5af4eb2a1b768bull),
+    __builtin_bit_cast(double, 0x3e927e500e0ac05bull), __builtin_bit_cast(double, 0x3ec71de01b889c29ull),
+    __builtin_bit_cast(double, 0x3efa01a0197bcfd8ull), __builtin_bit_cast(double, 0x3f2a01a01ac1a723ull),
+    __builtin_bit_cast(double, 0x3f56c16c16c18931ull), __builtin_bit_cast(double, 0x3f81111111110056ull),
+    __builtin_bit_cast(double, 0x3fa5555555555552ull), __builtin_bit_cast(double, 0x3fc5555555555557ull)};
+
+struct Expm1Reg {
+  double c[10];
+};
+
+__device__ __forceinline__ Expm1Reg expm1_regs() {
+  const int z = (int)__builtin_amdgcn_mbcnt_lo(0u, 0u);
+  Expm1Reg k;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) k.c[i] = kExpm1Coef[i + z];
+  return k;
+}
+
+__device__ __forceinline__ double expm1(double x, const Expm1Reg& k) {
+  const double n = __builtin_rint(x * c64(0x3ff71547652b82feull));
+  double r = __builtin_fma(c64(0xbfe62e42fefa39efull), n, x);
+  r = __builtin_fma(c64(0xbc7abc9e3b39803full), n, r);
+  double p = __builtin_fma(k.c[0], r, k.c[1]);
+#pragma unroll
+  for (int i = 2; i < 10; ++i) p = __builtin_fma(r, p, k.c[i]);
+  p = r * __builtin_fma(r, p, 0.5);
+  const bool top = (n == 1024.0);
+  const double s = top ? c64(0x7fe0000000000000ull) : __builtin_ldexp(1.0, (int)n);
+  const double t = s - 1.0;
+  const double u = __builtin_fma(r, p, r);
+  double y = __builtin_fma(s, u, t);
+  y = top ? y + y : y;
+  y = (x > c64(0x40862e42fefa39efull)) ? __builtin_inf() : y;
+  return (x < -37.0) ? -1.0 : y;
+}
+
 // a / b: LLVM's fp64 division core (rcp, two Newton-Raphson steps, quotient, one residual
 // correction) without the div_scale / div_fmas / div_fixup range guards.
 __device__ __forceinline__ double div(double a, double b) {

@@ -122,6 +122,40 @@ def test_single_sweep_from_identical_state_matches_oracle(fa):
         assert row_normwise(fdt, odt) < 1e-14
 
 
+def test_cold_layers_planck_overflow_matches_oracle(fa):
+    """Layers cold enough that hc/(lambda k T) passes 623 (expm1 >= 2^900: the sweep's
+    guard-free division hands those lanes to the IEEE one) and 709.78 (expm1 = inf, B = 0),
+    at short wavelengths: one sweep each way must still match the oracle strictly."""
+    rng = np.random.default_rng(17)
+    lam, _, _ = O.wavelength_grid(0.3, 10, 1024)
+    nL = 24
+    p = O.pressure_grid(nL, -6, np.log10(200))
+    T = np.geomspace(1500.0, 30.0, nL)            # bottom hot, top 30 K
+    x = O.H * O.C / (lam[None, :] * 1e-4 * O.K_B * T[:, None])
+    assert (x > 709.8).any() and ((x > 623.0) & (x < 709.7)).any()
+    Tn = np.linspace(0.9 * T.min(), 1.1 * T.max(), 9)
+    v = O.separable_table(10 ** rng.uniform(-2, 2, lam.size), (p / 1.0) ** 0.1,
+                          (Tn / 1000) ** 0.5)
+    tabs_o = {"1H2-16O": O.Table(v, p, Tn)}
+    tabs_f = {"1H2-16O": fa.OpacityTable(v, p, Tn)}
+    up0 = 10 ** rng.uniform(8, 12, (nL, lam.size))
+    down0 = 10 ** rng.uniform(6, 11, (nL, lam.size))
+    Ft = O.F_TOA(lam)
+    for kind in ("emit", "absorb"):
+        cond = _cond((nL, lam.size))
+        ofn = O.emit if kind == "emit" else O.absorb
+        with np.errstate(over="ignore", divide="ignore", invalid="ignore"):
+            ou, od, oT, odt, odT = ofn(tabs_o, T, p, lam, Ft, G_J, M_BAR, 1, up0.copy(),
+                                       down0.copy(), err=cond)
+        fn = fa.emit if kind == "emit" else fa.absorb
+        fu, fd, fT_, _, fdt, fdT = fn(tabs_f, T, p, lam, Ft, G_J, m_bar=M_BAR, n_timesteps=1,
+                                      fluxes_up=up0.copy(), fluxes_down=down0.copy())
+        assert np.isfinite(fu).all() and np.isfinite(fd).all()
+        assert_flux_parity(fu, ou, cond["up"], EPS, kind + " F_up (cold)")
+        assert_flux_parity(fd, od, cond["down"], EPS, kind + " F_down (cold)")
+        assert row_normwise(fdt, odt) < 1e-14
+
+
 def _grid_run(fa, C, pre, tabs_f, tabs_o, lam, p, T0, n, Ft=None):
     grid = fa.Grid(fa.Planet.from_hot_jupiter(), lam=lam, pressures=p, init_temperatures=T0)
     grid.load_opacities(opacities=tabs_f)

@@ -32,6 +32,10 @@ def main():
     builds = []
     for a in args:
         name, path = a.split("=", 1)
+        env = {}
+        if "@" in path:   # NAME=lib.so@VAR=v,VAR2=w: environment while the context is created
+            path, spec = path.split("@", 1)
+            env = dict(kv.split("=", 1) for kv in spec.split(","))
         q = None
         if ":" in path:
             path, q = path.rsplit(":", 1)
@@ -45,8 +49,11 @@ def main():
                 for s, n in enumerate(names)}
         if q is not None:
             os.environ["FREI_GROUP_Q"] = q
+        os.environ.update(env)
         eng = E.Engine(w["lam"], w["p"], tabs, mmr=w["mmr"][:S], device=0)
         os.environ.pop("FREI_GROUP_Q", None)
+        for k in env:
+            os.environ.pop(k, None)
         eng.state_init(w["T0"])
         eng.iterate(1)
         eng.synchronize()
