@@ -217,6 +217,7 @@ struct FastArgs {
   const int* conv;
   AtmStride bs;            // batched atmospheres (blockIdx.y of the sweep kernels)
   int n_atm;               // atmospheres in the launch (0 or 1: a single atmosphere)
+  int red_rows;            // one-lane sweep: per-row partial sums in LDS (fits: few layers)
 };
 
 struct SweepArgs {

@@ -175,7 +175,7 @@ __device__ __forceinline__ double rows_sum32(double x) {
 // of its residue q.  Every level is a DPP or permlane-swap VALU operation (the shfl form
 // costs one LDS round trip per level, which a one- or two-wave-per-SIMD slice cannot hide).
 // Fixed tree: deterministic.
-template <int Q>
+template <int Q, bool FULL = true>
 __device__ __forceinline__ double group_sum4(double q0, double q1, double q2, double q3,
                                              int lane) {
   const bool b = lane & Q;
@@ -191,6 +191,7 @@ __device__ __forceinline__ double group_sum4(double q0, double q1, double q2, do
   } else if constexpr (Q == 2) {
     y += dpp_bcast<0x128>(y);   // row_ror:8 (lane ^ 8)
   }
+  if constexpr (!FULL) return y;   // per-row sums: the caller adds the 4 rows later
   return rows_sum32(rows_sum16(y));
 }
 
@@ -389,6 +390,13 @@ struct PreCoef {
   double w0, dtau, B1, B2;
 };
 
+// LDS rows of per-step partial sums in the one-lane sweep: one per wave, or with
+// a.red_rows one per (wave, 16-lane row) — the wave sum then stops after the in-row DPP
+// levels (no permlane levels per step) and the block epilogue adds 4x more partials.
+__host__ __device__ inline int red_rows_per_block(int red_rows) {
+  return (kBlock / 64) * (red_rows ? 4 : 1);
+}
+
 template <int DIR, int S, int PD, bool NANCHK, bool SH>
 __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     FastArgs a, const FastStep* __restrict__ st, const FastStepS* __restrict__ ss,
@@ -424,7 +432,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   // K$ and L2 of a freshly scheduled CU (the step table was written by the update kernel).
   const FastStepS* sp = ss;
   if constexpr (SH) {
-    double* lss = red + (int64_t)(kBlock / 64) * ns * 4;
+    double* lss = red + (int64_t)red_rows_per_block(a.red_rows) * ns * 4;
     const double* g = reinterpret_cast<const double*>(ss);
     constexpr int kW = sizeof(FastStepS) / sizeof(double);
     for (int idx = tid; idx < ns * kW; idx += kBlock) lss[idx] = g[idx];
@@ -578,8 +586,16 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       if (st_dn) Fd[(int64_t)i * nl + j] = F1d;
       if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = c.dtau;
     }
-    const double y = wave_sum4(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
-    if (lane < 4) red[((int64_t)wv * ns + k) * 4 + (lane & 1) * 2 + ((lane >> 1) & 1)] = y;
+    // row sums (DPP only); lanes 0..3 of each 16-lane row write them, the block epilogue
+    // adds the 16 (wave, row) partials
+    const int qi = (lane & 1) * 2 + ((lane >> 1) & 1);
+    if (a.red_rows) {
+      const double y = group_sum4<1, false>(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
+      if ((lane & 15) < 4) red[((int64_t)(wv * 4 + (lane >> 4)) * ns + k) * 4 + qi] = y;
+    } else {
+      const double y = group_sum4<1>(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
+      if (lane < 4) red[((int64_t)wv * ns + k) * 4 + qi] = y;
+    }
     carry = (DIR == kEmit) ? F2u : F1d;
   };
 
@@ -615,10 +631,10 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     for (int b = 0; b < PD; ++b) finish(k + b, c[b]);
   }
   __syncthreads();
-  const int nw = kBlock / 64;
   for (int idx = tid; idx < ns * 4; idx += kBlock) {
     double s = red[idx];
-    for (int w = 1; w < nw; ++w) s += red[(int64_t)w * ns * 4 + idx];
+    for (int w = 1; w < red_rows_per_block(a.red_rows); ++w)
+      s += red[(int64_t)w * ns * 4 + idx];
     part[(int64_t)idx * gridDim.x + blockIdx.x] = s;
   }
 }
@@ -1439,7 +1455,7 @@ void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream
 
 template <int DIR, int S, int PD, bool NC, bool SH>
 static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
-  const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double) +
+  const size_t shm = (size_t)red_rows_per_block(a.red_rows) * a.n_steps * 4 * sizeof(double) +
                      (SH ? (size_t)a.n_steps * sizeof(FastStepS) : 0);
   hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC, SH>),
                      dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1), dim3(kBlock), shm,

@@ -166,6 +166,7 @@ struct frei_ctx {
   int pair_max_blocks = 640;            // FREI_PAIR_MAX_BLOCKS (<= 164k lambda per GPU)
   int quad_max_blocks = 128;            // FREI_QUAD_MAX_BLOCKS (<= 32k lambda per GPU)
   int group_q = 0;                      // FREI_GROUP_Q forces 1, 2 or 4 lanes per wavelength
+  int red_rows = 1;                     // FREI_RED_ROWS=0: full wave sums per step
   int depth4_max_blocks = 0;            // FREI_DEPTH4_MAX_BLOCKS (4 steps in flight: off, measured no faster)
   frei_allgather_fn host_ag = nullptr;  // host all-gather callback (alternative to RCCL)
   void* host_ag_user = nullptr;
@@ -478,6 +479,10 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     f.conv = c->d_conv;
     f.bs = atm_stride(c);
     f.n_atm = c->n_atm;
+    // per-row partials while the one-lane sweep's LDS stays within 48 KiB (3+ blocks per CU)
+    f.red_rows = c->red_rows &&
+                 (size_t)16 * ns * 4 * sizeof(double) + (size_t)ns * sizeof(FastStepS) <=
+                     48 * 1024;
     // Prefetch depth: below ~2 waves per SIMD (small per-GPU slices, e.g. 500k lambda over
     // 8 GPUs) a second layer in flight hides HBM latency; at full occupancy one suffices.
     // With one table (K3) and few blocks per CU, four steps in flight add the
@@ -642,6 +647,7 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
   if (const char* e = getenv("FREI_DEPTH4_MAX_BLOCKS")) c->depth4_max_blocks = atoi(e);
   if (const char* e = getenv("FREI_PAIR_MAX_BLOCKS")) c->pair_max_blocks = atoi(e);
   if (const char* e = getenv("FREI_QUAD_MAX_BLOCKS")) c->quad_max_blocks = atoi(e);
+  if (const char* e = getenv("FREI_RED_ROWS")) c->red_rows = atoi(e) != 0;
   if (const char* e = getenv("FREI_GROUP_Q")) {
     const int q = atoi(e);
     c->group_q = (q == 1 || q == 2 || q == 4) ? q : 0;
