@@ -692,7 +692,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   const int ns = a.n_steps;
   const fm::Expm1Reg ek = fm::expm1_regs();
   const double* __restrict__ tab = a.tab[0];
-  double* lss = red + (int64_t)(kBlock / 64) * ns * 4;
+  double* lss = red + (int64_t)red_rows_per_block(a.red_rows) * ns * 4;
   {
     const double* g = reinterpret_cast<const double*>(ss);
     constexpr int kW = sizeof(FastStepS) / sizeof(double);
@@ -810,10 +810,18 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
       if (st_dn) Fd[(int64_t)i * nl + j] = F1d;
       if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = c.dtau;
     }
-    const double y = group_sum4<Q>(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
     const int kq = (k - q) + (lane & (Q - 1));
-    if (lane < 4 * Q && kq < ns)
-      red[((int64_t)wv * ns + kq) * 4 + ((lane / Q) & 1) * 2 + ((lane / (2 * Q)) & 1)] = y;
+    if (a.red_rows) {   // per-row sums; the block epilogue adds the 16 (wave, row) partials
+      const double y = group_sum4<Q, false>(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
+      const int r = lane & 15;
+      if (r < 4 * Q && kq < ns)
+        red[((int64_t)(wv * 4 + (lane >> 4)) * ns + kq) * 4 + ((r / Q) & 1) * 2 +
+            ((r / (2 * Q)) & 1)] = y;
+    } else {
+      const double y = group_sum4<Q>(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
+      if (lane < 4 * Q && kq < ns)
+        red[((int64_t)wv * ns + kq) * 4 + ((lane / Q) & 1) * 2 + ((lane / (2 * Q)) & 1)] = y;
+    }
   };
   const int ng = (ns + Q - 1) / Q;
   double la, ha, sa, lb, hb, sb;   // two groups in flight
@@ -835,17 +843,17 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     if (g + 1 < ng) finish(A1, c1);
   }
   __syncthreads();
-  const int nw = kBlock / 64;
   for (int idx = tid; idx < ns * 4; idx += kBlock) {
     double s = red[idx];
-    for (int w = 1; w < nw; ++w) s += red[(int64_t)w * ns * 4 + idx];
+    for (int w = 1; w < red_rows_per_block(a.red_rows); ++w)
+      s += red[(int64_t)w * ns * 4 + idx];
     part[(int64_t)idx * gridDim.x + blockIdx.x] = s;
   }
 }
 
 // Q lanes per wavelength: kBlock / Q wavelengths per block.
 void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStream_t st) {
-  const size_t shm = (size_t)(kBlock / 64) * a.n_steps * 4 * sizeof(double) +
+  const size_t shm = (size_t)red_rows_per_block(a.red_rows) * a.n_steps * 4 * sizeof(double) +
                      (size_t)a.n_steps * sizeof(FastStepS);
   const dim3 grid(nblocks, a.n_atm > 1 ? a.n_atm : 1);
   if (Q == 4) {
