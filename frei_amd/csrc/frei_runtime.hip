@@ -344,7 +344,12 @@ int build_meta(frei_ctx* c) {
              q.p_nodes == q0.p_nodes && q.T_nodes == q0.T_nodes;
   }
   const bool small = c->nblocks <= c->shared_max_blocks;
-  c->shared = (c->shared_mode == 1 || (c->shared_mode < 0 && small)) ? shared : 0;
+  // the LDS-staged step table plus one partial-sum row per wave must leave room for several
+  // blocks per CU (deep atmospheres: > ~260 layers read the step table from global memory)
+  const size_t ns_l = (size_t)nL - 1;
+  const bool lds_fits =
+      (size_t)(kBlock / 64) * ns_l * 4 * sizeof(double) + ns_l * sizeof(FastStepS) <= 64 * 1024;
+  c->shared = (c->shared_mode == 1 || (c->shared_mode < 0 && small)) && lds_fits ? shared : 0;
   dfree(c->d_smeta);
   dfree(c->d_pmeta);
   dfree(c->d_tnodes);
