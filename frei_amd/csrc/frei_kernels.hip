@@ -701,16 +701,30 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   }
   const FastStepS* sp = reinterpret_cast<const FastStepS*>(lss);
   auto clampk = [&](int k) { return k < ns ? k : ns - 1; };
-  // loads of this lane's step in group g (step Qg + q, clamped for a dummy step)
-  auto load = [&](int g, double& vlo, double& vhi, double& stale) {
+  const int nL = ns + 1;
+  // A step's layer and top flag follow from its index (step_layer; emit's top step is the
+  // last), so only the bracket offset, weights, T and dm come from the LDS step table.
+  auto is_top = [&](int k) { return DIR == kEmit && k >= ns - 1; };
+  // Everything group g's phase A reads, issued together one group ahead: the LDS step
+  // parameters with the table rows and the stale flux (their latency overlaps).
+  struct Pre {
+    double vlo, vhi, stale, wl, wh, mm, dm, T;
+  };
+  auto load = [&](int g, Pre& P) {
     const int k = clampk(Q * g + q);
-    const double* r = tab + sp[k].off + j;
-    vlo = stream_load(r);
-    vhi = stream_load(r + a.pitch);
-    const int layer = sp[k].layer;
-    const double* src = (DIR == kEmit) ? (sp[k].top ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
+    const FastStepS& st = sp[k];
+    const double* r = tab + st.off + j;
+    P.wl = st.wlo;
+    P.wh = st.whi;
+    P.mm = st.mmr[0];
+    P.dm = st.dm;
+    P.T = DIR == kEmit ? st.T2 : st.T1;
+    P.vlo = stream_load(r);
+    P.vhi = stream_load(r + a.pitch);
+    const int layer = step_layer(DIR, k, nL);
+    const double* src = (DIR == kEmit) ? (is_top(k) ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
                                        : Fu + (int64_t)layer * nl;
-    stale = src[j];
+    P.stale = src[j];
   };
   double carry, carryB;
   {
@@ -729,19 +743,19 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   };
   // Phase A of this lane's step in group g (opacity, dtau, albedo, Planck chain of the
   // group); refills the group's buffer with group g + 2.
-  auto phaseA = [&](int g, double& vlo, double& vhi, double& stale, GroupA& A) {
+  auto phaseA = [&](int g, Pre& P, GroupA& A) {
     const int k = Q * g + q;
-    const FastStepS& st = sp[clampk(k)];
     A.k = k;
-    A.F_st = stale;
-    const double kap = st.mmr[0] * ((0.0 + vlo * st.wlo) + vhi * st.whi) + sig;
-    load(g + 2, vlo, vhi, stale);
-    A.dtau = st.dm * kap;
+    A.F_st = P.stale;
+    const double kap = P.mm * ((0.0 + P.vlo * P.wl) + P.vhi * P.wh) + sig;
+    const double dm = P.dm, Tnew = P.T;
+    load(g + 2, P);
+    A.dtau = dm * kap;
     A.w0 = fm::div(sig, sig + kap);
     // each lane forms its step's new Planck value; the group gathers them and resolves
     // (B1, B2) of its steps in order (emit: B2 is new and becomes the next B1; absorb: B1 is
     // new and becomes the next B2; emit's top step keeps B2 = B1)
-    const double X = planck(c1, lk, DIR == kEmit ? st.T2 : st.T1, ek);
+    const double X = planck(c1, lk, Tnew, ek);
     double Xr[Q], Bn[Q];
     Xr[0] = from_lane<Q, 0>(X);
     Xr[1] = from_lane<Q, 1>(X);
@@ -752,7 +766,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     double prev = carryB;
 #pragma unroll
     for (int r = 0; r < Q; ++r) {
-      const bool top = sp[clampk(Q * g + r)].top;
+      const bool top = is_top(Q * g + r);
       Bn[r] = (DIR == kEmit && top) ? prev : Xr[r];
       prev = Bn[r];
     }
@@ -802,10 +816,10 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     const double F2d = (DIR == kEmit) ? F_st : cin;
     const int k = A.k;
     if (act && k < ns) {
-      const FastStepS& st = sp[k];
-      const int i = st.layer;
-      const bool st_up = (DIR == kEmit) ? !st.top : (!a.live_only || i == 0);
-      const bool st_dn = (DIR == kAbsorb) || !a.live_only || st.top;
+      const int i = step_layer(DIR, k, nL);
+      const bool top = is_top(k);
+      const bool st_up = (DIR == kEmit) ? !top : (!a.live_only || i == 0);
+      const bool st_dn = (DIR == kAbsorb) || !a.live_only || top;
       if (st_up) Fu[(int64_t)(i + 1) * nl + j] = F2u;
       if (st_dn) Fd[(int64_t)i * nl + j] = F1d;
       if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = c.dtau;
@@ -824,13 +838,13 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     }
   };
   const int ng = (ns + Q - 1) / Q;
-  double la, ha, sa, lb, hb, sb;   // two groups in flight
-  load(0, la, ha, sa);
-  load(1, lb, hb, sb);
+  Pre pa, pb;                      // two groups in flight
+  load(0, pa);
+  load(1, pb);
   for (int g = 0; g < ng; g += 2) {
     GroupA A0, A1;
-    phaseA(g, la, ha, sa, A0);
-    phaseA(g + 1, lb, hb, sb, A1);   // a dummy group past the end is computed, not stored
+    phaseA(g, pa, A0);
+    phaseA(g + 1, pb, A1);   // a dummy group past the end is computed, not stored
     StepCoef c0, c1;
     if (__all(!(A0.w0 > 0.1) && !(A1.w0 > 0.1))) {
       coef_e1(A0.w0, A0.dtau, A0.B1, A0.B2, c0);
