@@ -449,11 +449,15 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
 #endif
   // Load the 2S table rows and the stale opposite-stream flux of step k into one buffer
   // (and, with shared brackets, the step's uniform parameters).
+  // a step's layer and top flag follow from its index (step_layer; emit's top step is the
+  // last one), so they need no step-table read
+  auto layer_of = [&](int k) { return step_layer(DIR, k, ns + 1); };
+  auto top_of = [&](int k) { return DIR == kEmit && k == ns - 1; };
   auto load = [&](int k, double (&v)[2 * S], double& stale) {
     k = k < ns ? k : ns - 1;  // unconditional (clamped) loads keep vmcnt waits counted
     if constexpr (SH) {
       const int64_t off = uni(sp[k].off);
-      const int layer = uni(sp[k].layer);
+      const int layer = layer_of(k);
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const double* r = a.tab[s] + off + j;
@@ -461,7 +465,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
         v[2 * s + 1] = stream_load(r + a.pitch);
       }
       const double* src = (DIR == kEmit)
-                              ? (uni(sp[k].top) ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
+                              ? (top_of(k) ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
                               : Fu + (int64_t)layer * nl;
       stale = src[j];
       return;
@@ -479,8 +483,8 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       v[2 * s + 1] = stream_load(r + a.pitch);
 #endif
     }
-    const int i = st[k].layer;
-    const double* src = (DIR == kEmit) ? (st[k].top ? a.ftoa : Fd + (int64_t)(i + 1) * nl)
+    const int i = layer_of(k);
+    const double* src = (DIR == kEmit) ? (top_of(k) ? a.ftoa : Fd + (int64_t)(i + 1) * nl)
                                        : Fu + (int64_t)i * nl;
     stale = src[j];
   };
@@ -492,14 +496,14 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     const int kk = k < ns ? k : ns - 1;  // the last pair of a PD = 2 loop may be a dummy
     double T1, T2, dm;
     if constexpr (SH) {
-      c.layer = uni(sp[kk].layer);
-      c.top = uni(sp[kk].top);
+      c.layer = layer_of(kk);
+      c.top = top_of(kk);
       T1 = UNIV(sp[kk].T1);
       T2 = UNIV(sp[kk].T2);
       dm = UNIV(sp[kk].dm);
     } else {
-      c.layer = st[kk].layer;
-      c.top = st[kk].top;
+      c.layer = layer_of(kk);
+      c.top = top_of(kk);
       T1 = st[kk].T1;
       T2 = st[kk].T2;
       dm = st[kk].dm;
