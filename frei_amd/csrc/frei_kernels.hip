@@ -793,29 +793,33 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   // the reduction of the group's bolometric terms.
   auto finish = [&](const GroupA& A, const StepCoef& c) {
     const double F_st = A.F_st;
-    auto recur = [&](double in, double& F2u, double& F1d) {
-      double F1u, F2d;
-      if (DIR == kEmit) { F1u = in; F2d = F_st; } else { F2d = in; F1u = F_st; }
-      F2u = c.ic * ((c.psi * F1u - c.xi * F2d) + c.Xu);
-      F1d = c.ic * ((c.psi * F2d - c.xi * F1u) + c.Xd);
+    // the two fluxes of a step from its carried input (same expressions as the one-lane form)
+    auto flux_up = [&](double in) {   // F_2_up
+      const double F1u = (DIR == kEmit) ? in : F_st, F2d = (DIR == kEmit) ? F_st : in;
+      return c.ic * ((c.psi * F1u - c.xi * F2d) + c.Xu);
     };
-    double cin = carry, F2u = 0.0, F1d = 0.0, in_r = carry;
+    auto flux_dn = [&](double in) {   // F_1_down
+      const double F1u = (DIR == kEmit) ? in : F_st, F2d = (DIR == kEmit) ? F_st : in;
+      return c.ic * ((c.psi * F2d - c.xi * F1u) + c.Xd);
+    };
+    // the carried chain runs through the group's steps in order, each step in its own lane
+    // (q == r); only the carried flux is formed in the chain, the other one once afterwards
+    double cin = carry, own = 0.0, in_r = carry;
 #pragma unroll
     for (int r = 0; r < Q; ++r) {
-      double a2u, a1d;
-      recur(in_r, a2u, a1d);            // meaningful in lane q == r
+      const double out = (DIR == kEmit) ? flux_up(in_r) : flux_dn(in_r);  // lane q == r
       if (q == r) {
         cin = in_r;
-        F2u = a2u;
-        F1d = a1d;
+        own = out;
       }
-      const double out = (DIR == kEmit) ? a2u : a1d;
       if (r == 0) in_r = from_lane<Q, 0>(out);
       else if (r == 1) in_r = from_lane<Q, 1>(out);
       else if (r == 2) in_r = from_lane<Q, (Q == 4 ? 2 : 0)>(out);
       else in_r = from_lane<Q, (Q == 4 ? 3 : 0)>(out);
     }
     carry = in_r;
+    const double F2u = (DIR == kEmit) ? own : flux_up(cin);
+    const double F1d = (DIR == kEmit) ? flux_dn(cin) : own;
     const double F1u = (DIR == kEmit) ? cin : F_st;
     const double F2d = (DIR == kEmit) ? F_st : cin;
     const int k = A.k;
