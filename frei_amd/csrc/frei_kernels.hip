@@ -789,6 +789,12 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     }
     carryB = Bn[Q - 1];
   };
+  // This lane's flux / dtau row pointers for its step of the current group: Q rows on per
+  // group (up for emit, down for absorb), so the stores need no per-step row arithmetic.
+  const int64_t rstep = (DIR == kEmit ? (int64_t)Q : -(int64_t)Q) * nl;
+  double* pu = Fu + (int64_t)(step_layer(DIR, q, nL) + 1) * nl + j;
+  double* pd = Fd + (int64_t)step_layer(DIR, q, nL) * nl + j;
+  double* pt = (dtaus ? dtaus : Fu) + (int64_t)(q + 1) * nl + j;
   // Carried recurrence through the group (steps in order), stores of this lane's step and
   // the reduction of the group's bolometric terms.
   auto finish = [&](const GroupA& A, const StepCoef& c) {
@@ -808,7 +814,9 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
 #pragma unroll
     for (int r = 0; r < Q; ++r) {
       const double out = (DIR == kEmit) ? flux_up(in_r) : flux_dn(in_r);  // lane q == r
-      if (q == r) {
+      if (r == 0) {
+        own = out;
+      } else if (q == r) {
         cin = in_r;
         own = out;
       }
@@ -824,14 +832,17 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     const double F2d = (DIR == kEmit) ? F_st : cin;
     const int k = A.k;
     if (act && k < ns) {
-      const int i = step_layer(DIR, k, nL);
-      const bool top = is_top(k);
-      const bool st_up = (DIR == kEmit) ? !top : (!a.live_only || i == 0);
-      const bool st_dn = (DIR == kAbsorb) || !a.live_only || top;
-      if (st_up) Fu[(int64_t)(i + 1) * nl + j] = F2u;
-      if (st_dn) Fd[(int64_t)i * nl + j] = F1d;
-      if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = c.dtau;
+      // emit's top step and absorb's bottom step are both the last step (k = ns - 1)
+      const bool last = k == ns - 1;
+      const bool st_up = (DIR == kEmit) ? !last : (!a.live_only || last);
+      const bool st_dn = (DIR == kAbsorb) || !a.live_only || last;
+      if (st_up) *pu = F2u;
+      if (st_dn) *pd = F1d;
+      if (dtaus) *pt = c.dtau;
     }
+    pu += rstep;
+    pd += rstep;
+    pt += (int64_t)Q * nl;
     const int kq = (k - q) + (lane & (Q - 1));
     if (a.red_rows) {   // per-row sums; the block epilogue adds the 16 (wave, row) partials
       const double y = group_sum4<Q, false>(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
