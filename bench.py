@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--no-binning", action="store_true",
                     help="skip the K6 opacity-binning measurement (rank 0)")
     ap.add_argument("--binning-reps", type=int, default=5)
+    ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
+                    help="N > 1 exchange: RCCL all-gather (default) or the host (gloo) hook; "
+                         "host lets several ranks share one GPU to rehearse the multi-rank flow")
     ap.add_argument("--no-c5", action="store_true",
                     help="skip the batched-atmosphere (C5) measurement")
     ap.add_argument("--c5-lam", type=int, default=100_000)
@@ -62,7 +65,16 @@ class Dist:
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
-            dist.init_process_group("gloo")
+            # gloo announces its connections on stdout; keep stdout for the one JSON line
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo")
+                dist.barrier()
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.dist = dist
 
     def barrier(self):
@@ -226,11 +238,16 @@ def main():
     from frei_amd.opacity import SeparableTable
     from frei_amd.workloads import bytes_per_update, c3
 
+    if a.comm == "host":   # rehearsal: ranks may share the GPUs there are
+        d.local = d.local % max(1, N.device_count())
     w = c3(n_layers=a.n_layers, n_lam=a.n_lam, n_T=a.n_T)
     nL, n_lam, S = a.n_layers, a.n_lam, len(w["names"])
     lo, hi = partition(n_lam, d.world, d.rank)
     comm = None
-    if d.world > 1:
+    if d.world > 1 and a.comm == "host":
+        from frei_amd.distributed import gloo_comm
+        comm = gloo_comm(d.dist, d.world, d.rank)
+    elif d.world > 1:
         uid = None
         if d.rank == 0:
             import ctypes
@@ -335,7 +352,9 @@ def main():
                                    f"(H2O/CO/CO2/CH4/Na/K + H2-H2/H2-He CIA), {a.n_T} T-nodes, "
                                    "1 step = 1 T-P iteration (emit+absorb)",
                        "n_layers": nL, "n_lambda": n_lam, "n_species": S, "n_T": a.n_T,
-                       "parallelism": f"lambda-shard x{d.world} (RCCL all-gather per sweep)"},
+                       "parallelism": f"lambda-shard x{d.world} "
+                                      + ("(RCCL all-gather per sweep)" if a.comm == "rccl"
+                                         else "(host all-gather per sweep, rehearsal)")},
             "tp_iters_per_s": 1e3 / ms_per_step,
             "sweep_path": dict(path, setup_ms=setup_ms,
                                note="setup_ms: one-time metadata build + species contraction "
