@@ -65,16 +65,7 @@ class Dist:
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
-            # gloo announces its connections on stdout; keep stdout for the one JSON line
-            saved = os.dup(1)
-            os.dup2(2, 1)
-            try:
-                dist.init_process_group("gloo")
-                dist.barrier()
-            finally:
-                sys.stdout.flush()
-                os.dup2(saved, 1)
-                os.close(saved)
+            dist.init_process_group("gloo")   # its notices go to stderr (_reserve_stdout)
             self.dist = dist
 
     def barrier(self):
@@ -230,7 +221,24 @@ def c5_leg(a, d):
             "note": "setup_s: table generation + metadata + K7 MFMA contraction, once"}
 
 
+# stdout carries exactly one line: the JSON result of rank 0.  Everything else any library
+# writes to fd 1 (gloo's connection notices, RCCL, the HIP runtime) goes to stderr.
+_RESULT_FD = None
+
+
+def _reserve_stdout():
+    global _RESULT_FD
+    sys.stdout.flush()
+    _RESULT_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def _emit_result(line):
+    os.write(_RESULT_FD, (json.dumps(line) + "\n").encode())
+
+
 def main():
+    _reserve_stdout()
     a = parse()
     d = Dist(a.gpus)
     from frei_amd import _native as N
@@ -380,7 +388,7 @@ def main():
             "k6_binning": binning,
             "c5_batched": c5,
         }
-        print(json.dumps(line), flush=True)
+        _emit_result(line)
 
 
 if __name__ == "__main__":
