@@ -288,19 +288,6 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
 #ifndef FREI_NT
 #define FREI_NT 0
 #endif
-#ifndef FREI_PAIRLOAD
-#define FREI_PAIRLOAD 0  // paired 16 B loads: same bandwidth, +64 VALU selects/DPP per layer
-#endif
-
-// Swap a double with the neighbouring lane (lane ^ 1) through DPP quad_perm [1,0,3,2]:
-// a VALU move, no LDS round trip.
-__device__ __forceinline__ double swap_pair(double x) {
-  const int2 v = __builtin_bit_cast(int2, x);
-  int2 r;
-  r.x = __builtin_amdgcn_mov_dpp(v.x, 0xB1, 0xF, 0xF, false);
-  r.y = __builtin_amdgcn_mov_dpp(v.y, 0xB1, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, r);
-}
 __device__ __forceinline__ double stream_load(const double* p) {
 #if FREI_NT
   return __builtin_nontemporal_load(p);
@@ -439,14 +426,6 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     __syncthreads();
     sp = reinterpret_cast<const FastStepS*>(lss);
   }
-#if FREI_PAIRLOAD
-  // Lane pair (2m, 2m+1) covers wavelengths (2m, 2m+1): the even lane loads the T_lo row,
-  // the odd lane the T_hi row, 16 B each (global_load_dwordx4, 1 KiB per wave-instruction);
-  // one DPP swap later gives every lane both rows at its own wavelength.
-  const bool odd = lane & 1;
-  const int64_t jp = j0 & ~(int64_t)1;   // pair base (rows are padded: jp + 1 < row pitch)
-  const int64_t pitch = a.pitch;
-#endif
   // Load the 2S table rows and the stale opposite-stream flux of step k into one buffer
   // (and, with shared brackets, the step's uniform parameters).
   // a step's layer and top flag follow from its index (step_layer; emit's top step is the
@@ -472,16 +451,9 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-#if FREI_PAIRLOAD
-      const double2 q = *reinterpret_cast<const double2*>(
-          a.tab[s] + st[k].off[s] + (odd ? pitch : 0) + jp);
-      v[2 * s] = q.x;
-      v[2 * s + 1] = q.y;
-#else
       const double* r = a.tab[s] + st[k].off[s] + j;
       v[2 * s] = stream_load(r);
       v[2 * s + 1] = stream_load(r + a.pitch);
-#endif
     }
     const int i = layer_of(k);
     const double* src = (DIR == kEmit) ? (top_of(k) ? a.ftoa : Fd + (int64_t)(i + 1) * nl)
@@ -511,13 +483,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     double tot = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-#if FREI_PAIRLOAD
-      const double recv = swap_pair(odd ? v[2 * s] : v[2 * s + 1]);
-      const double vlo = odd ? recv : v[2 * s];
-      const double vhi = odd ? v[2 * s + 1] : recv;
-#else
       const double vlo = v[2 * s], vhi = v[2 * s + 1];
-#endif
       double ops;
       if constexpr (SH) {
         ops = UNIV(sp[kk].mmr[s]) * ((0.0 + vlo * UNIV(sp[kk].wlo)) + vhi * UNIV(sp[kk].whi));

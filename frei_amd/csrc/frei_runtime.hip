@@ -161,8 +161,8 @@ struct frei_ctx {
   // FREI_SHARED=0/1 forces it off/on; FREI_SHARED_MAX_BLOCKS moves the threshold.
   int shared_mode = -1;
   int shared_max_blocks = 1024;
-  // Paired-lane sweep (two lanes per wavelength): contracted table, LDS step table and at
-  // most this many 256-wavelength blocks, i.e. about one wave per SIMD or less.
+  // Grouped-lane sweep (2 or 4 lanes per wavelength): contracted table, LDS step table and
+  // at most this many 256-wavelength blocks, i.e. about one wave per SIMD or less.
   int pair_max_blocks = 640;            // FREI_PAIR_MAX_BLOCKS (<= 164k lambda per GPU)
   int quad_max_blocks = 128;            // FREI_QUAD_MAX_BLOCKS (<= 32k lambda per GPU)
   int group_q = 0;                      // FREI_GROUP_Q forces 1, 2 or 4 lanes per wavelength
