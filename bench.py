@@ -289,7 +289,15 @@ def main():
     eng.iterate(max(2, a.steps // 2))
     eng.synchronize()
     sweep_ms, n_sweeps = eng.timing_read()
+    xch_ms, n_xch = eng.timing_read_exchange()
     eng.timing(False)
+    exchange = None
+    if d.world > 1:   # per-sweep rank exchange (HIP events on the engine stream), max over ranks
+        exchange = {"kind": ("RCCL all-gather" if a.comm == "rccl" else "host all-gather")
+                            + f" of {4 * (nL - 1) * 8} B per rank",
+                    "avg_ms": d.max(xch_ms / max(n_xch, 1)), "calls": n_xch,
+                    "note": "stream time from the start of the exchange to the end of the "
+                            "all-gather, per sweep (includes waiting for the slowest rank)"}
     updates_per_step = 2 * (nL - 1) * n_lam
     value = updates_per_step * a.steps / elapsed
     ms_per_step = elapsed / a.steps * 1e3
@@ -364,6 +372,7 @@ def main():
                                       + ("(RCCL all-gather per sweep)" if a.comm == "rccl"
                                          else "(host all-gather per sweep, rehearsal)")},
             "tp_iters_per_s": 1e3 / ms_per_step,
+            "exchange": exchange,
             "sweep_path": dict(path, setup_ms=setup_ms,
                                note="setup_ms: one-time metadata build + species contraction "
                                     "(K3) per tables/mmr, outside the timed steps"),

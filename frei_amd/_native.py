@@ -68,6 +68,7 @@ SIGNATURES = {
     "frei_contribution": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, ctypes.c_double, _dp]),
     "frei_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "frei_timing_read": (ctypes.c_int, [_vp, _dp, _ip]),
+    "frei_timing_read_exchange": (ctypes.c_int, [_vp, _dp, _ip]),
     "frei_xsec_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, _fp, ctypes.c_int,
                                         ctypes.c_int, _i64, _dp, _dp, _dp]),
     "frei_xsec_create_synthetic": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int,

@@ -175,6 +175,8 @@ struct frei_ctx {
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
+  std::vector<hipEvent_t> xev_pool;     // around the rank exchange (all-gather) of each sweep
+  size_t xev_used = 0;
 };
 
 namespace {
@@ -407,14 +409,15 @@ SetupArgs setup_args(frei_ctx* c) {
   return u;
 }
 
-hipEvent_t next_event(frei_ctx* c) {
-  if (c->ev_used == c->ev_pool.size()) {
+hipEvent_t next_event_in(std::vector<hipEvent_t>& pool, size_t& used) {
+  if (used == pool.size()) {
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) return nullptr;
-    c->ev_pool.push_back(e);
+    pool.push_back(e);
   }
-  return c->ev_pool[c->ev_used++];
+  return pool[used++];
 }
+hipEvent_t next_event(frei_ctx* c) { return next_event_in(c->ev_pool, c->ev_used); }
 
 struct SweepOpts {
   int dir = kEmit;
@@ -516,6 +519,13 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   }
   HIP_TRY(hipGetLastError());
   const double* Fb = c->d_Fb;
+  hipEvent_t x1 = nullptr;
+  if (c->timing && (c->comm || (c->nranks > 1 && c->host_ag))) {   // exchange timing
+    hipEvent_t x0 = next_event_in(c->xev_pool, c->xev_used);
+    x1 = next_event_in(c->xev_pool, c->xev_used);
+    if (!x0 || !x1) return fail("hipEventCreate failed");
+    HIP_TRY(hipEventRecord(x0, c->stream));
+  }
   if (c->nranks > 1 && c->host_ag) {
     const size_t n = (size_t)ns * 4;
     HIP_TRY(hipMemcpyAsync(c->h_ag, c->d_Fb, n * sizeof(double), hipMemcpyDeviceToHost,
@@ -535,6 +545,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
       return fail(std::string("ncclAllGather: ") + (r->errStr ? r->errStr(rc) : "error"));
     Fb = c->d_Fb_all;
   }
+  if (x1) HIP_TRY(hipEventRecord(x1, c->stream));
   UpdateArgs u{};
   u.su = setup_args(c);
   u.dir = o.dir;
@@ -734,6 +745,7 @@ int frei_ctx_destroy(frei_ctx* c) {
   if (c->h_ag) (void)hipHostFree(c->h_ag);
   for (auto e : c->flag_ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto e : c->xev_pool) (void)hipEventDestroy(e);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1355,6 +1367,7 @@ int frei_timing_enable(frei_ctx* c, int on) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->timing = on != 0;
   c->ev_used = 0;
+  c->xev_used = 0;
   return 0;
 }
 
@@ -1370,6 +1383,21 @@ int frei_timing_read(frei_ctx* c, double* total_ms, int* n_launches) {
   }
   *total_ms = tot;
   *n_launches = (int)(c->ev_used / 2);
+  return 0;
+}
+
+int frei_timing_read_exchange(frei_ctx* c, double* total_ms, int* n_calls) {
+  if (!c || !total_ms || !n_calls) return fail("null argument");
+  TRY(set_device(c));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  double tot = 0;
+  for (size_t k = 0; k + 1 < c->xev_used; k += 2) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, c->xev_pool[k], c->xev_pool[k + 1]));
+    tot += ms;
+  }
+  *total_ms = tot;
+  *n_calls = (int)(c->xev_used / 2);
   return 0;
 }
 

@@ -236,6 +236,12 @@ class Engine:
         N.check(N.lib().frei_timing_read(self._ctx, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def timing_read_exchange(self):
+        """(total ms, calls) of the timed rank exchanges (all-gathers) since timing(True)."""
+        ms, n = ctypes.c_double(), ctypes.c_int()
+        N.check(N.lib().frei_timing_read_exchange(self._ctx, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
     def milne_pressure(self, p_bar, dtaus=None):
         """Per-wavelength Milne pressures of this slice (core.py:392-395) from ``dtaus`` (host
         array) or, with None, the dtaus the last run left on the device."""

@@ -193,6 +193,9 @@ int frei_ctx_path(frei_ctx* ctx, int* flags);
  * launch while enabled): total milliseconds and number of timed launches. */
 int frei_timing_enable(frei_ctx* ctx, int on);
 int frei_timing_read(frei_ctx* ctx, double* total_ms, int* n_launches);
+/* While timing is enabled, also HIP events around each sweep's rank exchange (the RCCL
+ * all-gather of the bolometric partials, or the host hook): total ms and number of calls. */
+int frei_timing_read_exchange(frei_ctx* ctx, double* total_ms, int* n_calls);
 
 /*
  * Opacity binning (opacity.py:66-170).  A frei_xsec is one species' high-resolution
