@@ -192,6 +192,40 @@ def test_deep_atmosphere_sweeps_match_oracle(fa):
         assert row_normwise(fdt, odt) < 1e-14
 
 
+@pytest.mark.parametrize("n_lam,nL,S", [(3, 4, 1), (63, 5, 2), (65, 7, 1), (129, 33, 3),
+                                         (257, 6, 2), (1000, 9, 1)])
+def test_ragged_shapes_sweeps_match_oracle(fa, n_lam, nL, S):
+    """Edge shapes: wavelength counts around the 64/128/256-lane block sizes of the one-lane
+    and grouped-lane sweeps, the fewest layers, odd step counts; one sweep each way."""
+    rng = np.random.default_rng(1000 * n_lam + nL)
+    lam, _, _ = O.wavelength_grid(0.5, 10, n_lam)
+    p = O.pressure_grid(nL, -6, np.log10(200))
+    T = O.temperature_grid(p, 1700.0, 0.1, 0.1) * (1 + 0.03 * rng.standard_normal(nL))
+    Tn = np.linspace(0.7 * T.min(), 1.3 * T.max(), 5)
+    names = ["1H2-16O", "12C-16O", "Na"][:S]
+    tabs_o, tabs_f = {}, {}
+    for n in names:
+        v = O.separable_table(10 ** rng.uniform(-3, 2, lam.size), (p / 1.0) ** 0.1,
+                              (Tn / 1000) ** 0.5)
+        tabs_o[n] = O.Table(v, p, Tn)
+        tabs_f[n] = fa.OpacityTable(v, p, Tn)
+    up0 = 10 ** rng.uniform(8, 12, (nL, lam.size))
+    down0 = 10 ** rng.uniform(6, 11, (nL, lam.size))
+    Ft = O.F_TOA(lam)
+    for kind in ("emit", "absorb"):
+        cond = _cond((nL, lam.size))
+        ofn = O.emit if kind == "emit" else O.absorb
+        ou, od, oT, odt, odT = ofn(tabs_o, T, p, lam, Ft, G_J, M_BAR, 1, up0.copy(),
+                                   down0.copy(), err=cond)
+        fn = fa.emit if kind == "emit" else fa.absorb
+        fu, fd, fT_, _, fdt, fdT = fn(tabs_f, T, p, lam, Ft, G_J, m_bar=M_BAR, n_timesteps=1,
+                                      fluxes_up=up0.copy(), fluxes_down=down0.copy())
+        assert_flux_parity(fu, ou, cond["up"], EPS, f"{kind} F_up {n_lam}x{nL}")
+        assert_flux_parity(fd, od, cond["down"], EPS, f"{kind} F_down {n_lam}x{nL}")
+        assert rel(fT_, oT) < 1e-10
+        assert row_normwise(fdt, odt) < 1e-14
+
+
 def _grid_run(fa, C, pre, tabs_f, tabs_o, lam, p, T0, n, Ft=None):
     grid = fa.Grid(fa.Planet.from_hot_jupiter(), lam=lam, pressures=p, init_temperatures=T0)
     grid.load_opacities(opacities=tabs_f)
