@@ -1,0 +1,72 @@
+"""Full-size (C3: 60 layers x 500k lambda x 8 species) properties on the GPU.
+
+The oracle cannot run 500k wavelengths in test time, so at BASELINE.json's full size the
+checks are size-independent properties of the path:
+- determinism: two runs give bitwise identical temperatures, spectra and dtaus;
+- the grouped-lane sweep (2 lanes per wavelength, forced) against the one-lane sweep the
+  full slice uses: temperatures within 1e-12 (only the bolometric summation tree differs);
+- the species contraction (K3) against the per-species sum in the sweep: within the
+  parity tolerance (the species sum is reordered);
+- physical sanity: finite, positive fluxes and a spectrum that responds to T.
+"""
+import numpy as np
+import pytest
+
+from tests.parity import rel
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(monkeypatch, env):
+    import frei_amd as fa
+    from frei_amd.workloads import c3
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    w = c3()
+    tabs = {n: fa.SeparableTable(w["base"][s], w["fp"][s], w["fT"][s], w["p"], w["T_nodes"])
+            for s, n in enumerate(w["names"])}
+    eng = fa.Engine(w["lam"], w["p"], tabs, mmr=w["mmr"])
+    for k in env:
+        monkeypatch.delenv(k)
+    return eng, w
+
+
+def _run(eng, w, n=6):
+    out = eng.run(w["T0"], n_timesteps=n, n_zero_crossings=10 ** 6, convergence_dT=-1.0)
+    return out
+
+
+def test_full_size_properties(monkeypatch):
+    runs = {}
+    variants = (("default", {}), ("again", {}),
+                ("pair", {"FREI_GROUP_Q": "2", "FREI_SHARED_MAX_BLOCKS": "100000"}),
+                ("per_species", {"FREI_PRECONTRACT": "0"}))
+    for name, env in variants:
+        eng, w = _engine(monkeypatch, env)
+        try:
+            path = eng.path()
+            if name == "pair":
+                assert path["paired"]
+            if name == "per_species":
+                assert not path["contracted"]
+            else:
+                assert path["contracted"]
+            runs[name] = _run(eng, w)
+        finally:
+            eng.close()
+    a, b = runs["default"], runs["again"]
+    assert np.array_equal(a["final_T"], b["final_T"])
+    assert np.array_equal(a["spectrum"], b["spectrum"])
+    assert np.array_equal(a["dtaus"], b["dtaus"])
+    assert np.isfinite(a["spectrum"]).all() and (a["spectrum"] > 0).all()
+    assert np.isfinite(a["dtaus"]).all()
+    assert rel(runs["pair"]["final_T"], a["final_T"]) < 1e-12
+    assert rel(runs["pair"]["spectrum"], a["spectrum"]) < 1e-9
+    assert rel(runs["per_species"]["final_T"], a["final_T"]) < 1e-10
+    # the T-P loop moved the temperatures (6 iterations from the initial profile)
+    assert rel(a["final_T"], w_T0()) > 1e-6
+
+
+def w_T0():
+    from frei_amd.workloads import c3
+    return c3(n_lam=1000)["T0"]
