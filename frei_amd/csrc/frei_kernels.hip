@@ -377,11 +377,23 @@ struct PreCoef {
   double w0, dtau, B1, B2;
 };
 
-// LDS rows of per-step partial sums in the one-lane sweep: one per wave, or with
-// a.red_rows one per (wave, 16-lane row) — the wave sum then stops after the in-row DPP
-// levels (no permlane levels per step) and the block epilogue adds 4x more partials.
+// Per-step partial sums in LDS (a.red_rows):
+//   0  one row per wave: a full DPP/permlane wave sum per step;
+//   1  one row per (wave, 16-lane row): the wave sum stops after the in-row DPP levels and
+//      the block epilogue adds 4x more partials;
+//   2  (one-lane sweep, two steps in flight) staged: each lane parks its 4 weighted values
+//      of both steps in a per-wave LDS tile; then every lane sums 8 consecutive lanes of one
+//      of the 8 (step, quantity) outputs and three DPP levels finish the 64-lane sums —
+//      about a third of the VALU work of a per-step butterfly, no block barrier.
 __host__ __device__ inline int red_rows_per_block(int red_rows) {
-  return (kBlock / 64) * (red_rows ? 4 : 1);
+  return (kBlock / 64) * (red_rows == 1 ? 4 : 1);
+}
+// mode 2 tile: [wave][2 steps][4 quantities][64 lanes + 8 pad]; the pad staggers the rows
+// over the LDS banks so the strided reads of the reduction are conflict-free
+constexpr int kStageRow = 72;
+constexpr int kStageDoubles = (kBlock / 64) * 2 * 4 * kStageRow;
+__host__ __device__ inline int64_t red_lds_doubles(int red_rows, int ns) {
+  return (int64_t)red_rows_per_block(red_rows) * ns * 4 + (red_rows == 2 ? kStageDoubles : 0);
 }
 
 template <int DIR, int S, int PD, bool NANCHK, bool SH>
@@ -419,7 +431,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   // K$ and L2 of a freshly scheduled CU (the step table was written by the update kernel).
   const FastStepS* sp = ss;
   if constexpr (SH) {
-    double* lss = red + (int64_t)red_rows_per_block(a.red_rows) * ns * 4;
+    double* lss = red + red_lds_doubles(a.red_rows, ns);
     const double* g = reinterpret_cast<const double*>(ss);
     constexpr int kW = sizeof(FastStepS) / sizeof(double);
     for (int idx = tid; idx < ns * kW; idx += kBlock) lss[idx] = g[idx];
@@ -556,6 +568,16 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       if (st_dn) Fd[(int64_t)i * nl + j] = F1d;
       if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = c.dtau;
     }
+    if (PD == 2 && a.red_rows == 2) {   // staged: reduced per pair of steps (stage_reduce)
+      double* t = red + (int64_t)(kBlock / 64) * ns * 4 + ((wv * 2 + (k & 1)) * 4) * kStageRow +
+                  lane;
+      t[0] = wt * F2u;
+      t[kStageRow] = wt * F2d;
+      t[2 * kStageRow] = wt * F1u;
+      t[3 * kStageRow] = wt * F1d;
+      carry = (DIR == kEmit) ? F2u : F1d;
+      return;
+    }
     // row sums (DPP only); lanes 0..3 of each 16-lane row write them, the block epilogue
     // adds the 16 (wave, row) partials
     const int qi = (lane & 1) * 2 + ((lane >> 1) & 1);
@@ -599,6 +621,24 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     coefB(pc, c);
 #pragma unroll
     for (int b = 0; b < PD; ++b) finish(k + b, c[b]);
+    if constexpr (PD == 2) {
+      if (a.red_rows == 2) {   // the pair's 8 (step, quantity) sums over the wave's 64 lanes
+        __builtin_amdgcn_wave_barrier();
+        const int o = lane >> 3;
+        // lane r = lane & 7 of output o sums lanes r, r + 8, ..., r + 56 of that output's row
+        const double* t = red + (int64_t)(kBlock / 64) * ns * 4 +
+                          ((wv * 2 + (o >> 2)) * 4 + (o & 3)) * kStageRow + (lane & 7);
+        double y = t[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) y += t[8 * i];
+        y += dpp_bcast<0xB1>(y);    // quad_perm [1,0,3,2]
+        y += dpp_bcast<0x4E>(y);    // quad_perm [2,3,0,1]
+        y += dpp_bcast<0x141>(y);   // row_half_mirror: the other quad of the 8-lane group
+        const int ks = k + (o >> 2);
+        if ((lane & 7) == 0 && ks < ns) red[((int64_t)wv * ns + ks) * 4 + (o & 3)] = y;
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
   }
   __syncthreads();
   for (int idx = tid; idx < ns * 4; idx += kBlock) {
@@ -1462,7 +1502,7 @@ void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream
 
 template <int DIR, int S, int PD, bool NC, bool SH>
 static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
-  const size_t shm = (size_t)red_rows_per_block(a.red_rows) * a.n_steps * 4 * sizeof(double) +
+  const size_t shm = (size_t)red_lds_doubles(a.red_rows, a.n_steps) * sizeof(double) +
                      (SH ? (size_t)a.n_steps * sizeof(FastStepS) : 0);
   hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC, SH>),
                      dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1), dim3(kBlock), shm,

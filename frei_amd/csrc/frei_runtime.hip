@@ -167,6 +167,7 @@ struct frei_ctx {
   int quad_max_blocks = 128;            // FREI_QUAD_MAX_BLOCKS (<= 32k lambda per GPU)
   int group_q = 0;                      // FREI_GROUP_Q forces 1, 2 or 4 lanes per wavelength
   int red_rows = 1;                     // FREI_RED_ROWS=0: full wave sums per step
+  int red_stage = 1;                    // FREI_RED_STAGE=0: no staged sums (one-lane sweep)
   int depth4_max_blocks = 0;            // FREI_DEPTH4_MAX_BLOCKS (4 steps in flight: off, measured no faster)
   frei_allgather_fn host_ag = nullptr;  // host all-gather callback (alternative to RCCL)
   void* host_ag_user = nullptr;
@@ -500,6 +501,11 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     bool nan_check = false;
     for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
     const int Q = group_lanes(c);
+    // staged partial sums (mode 2) for the one-lane sweep with two steps in flight
+    if (Q == 1 && depth == 2 && c->red_stage &&
+        ((size_t)(kBlock / 64) * ns * 4 + (size_t)(kBlock / 64) * 2 * 4 * 72) * sizeof(double) +
+                (size_t)ns * sizeof(FastStepS) <= 48 * 1024)
+      f.red_rows = 2;
     if (Q > 1) {
       nb_run = (int)((c->nlam + kBlock / Q - 1) / (kBlock / Q));
       launch_sweep_group(o.dir, Q, f, nb_run, c->stream);
@@ -664,6 +670,7 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
   if (const char* e = getenv("FREI_PAIR_MAX_BLOCKS")) c->pair_max_blocks = atoi(e);
   if (const char* e = getenv("FREI_QUAD_MAX_BLOCKS")) c->quad_max_blocks = atoi(e);
   if (const char* e = getenv("FREI_RED_ROWS")) c->red_rows = atoi(e) != 0;
+  if (const char* e = getenv("FREI_RED_STAGE")) c->red_stage = atoi(e) != 0;
   if (const char* e = getenv("FREI_GROUP_Q")) {
     const int q = atoi(e);
     c->group_q = (q == 1 || q == 2 || q == 4) ? q : 0;
