@@ -702,7 +702,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   const int ns = a.n_steps;
   const fm::Expm1Reg ek = fm::expm1_regs();
   const double* __restrict__ tab = a.tab[0];
-  double* lss = red + (int64_t)red_rows_per_block(a.red_rows) * ns * 4;
+  double* lss = red + red_lds_doubles(a.red_rows, ns);
   {
     const double* g = reinterpret_cast<const double*>(ss);
     constexpr int kW = sizeof(FastStepS) / sizeof(double);
@@ -849,6 +849,15 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     pu += rstep;
     pd += rstep;
     pt += (int64_t)Q * nl;
+    if (a.red_rows == 2) {   // staged: reduced per pair of groups (below, main loop)
+      double* t = red + (int64_t)(kBlock / 64) * ns * 4 +
+                  ((wv * 2 + ((k / Q) & 1)) * 4) * kStageRow + lane;
+      t[0] = wt * F2u;
+      t[kStageRow] = wt * F2d;
+      t[2 * kStageRow] = wt * F1u;
+      t[3 * kStageRow] = wt * F1d;
+      return;
+    }
     const int kq = (k - q) + (lane & (Q - 1));
     if (a.red_rows) {   // per-row sums; the block epilogue adds the 16 (wave, row) partials
       const double y = group_sum4<Q, false>(wt * F2u, wt * F2d, wt * F1u, wt * F1d, lane);
@@ -880,6 +889,26 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     }
     finish(A0, c0);
     if (g + 1 < ng) finish(A1, c1);
+    if (a.red_rows == 2) {
+      // the 8Q (group, quantity, step residue) sums of the two groups over the wave's 64/Q
+      // wavelengths: 8/Q lanes per output, each adds 8 staged values (residue qq, lanes
+      // qq + Q r + 8 i), then DPP finishes over the 8/Q lanes
+      __builtin_amdgcn_wave_barrier();
+      constexpr int L = 8 / Q;                       // lanes per output
+      const int o = lane / L, r = lane % L;
+      const int p = o / (4 * Q), qi = (o / Q) & 3, qq = o % Q;
+      const double* t = red + (int64_t)(kBlock / 64) * ns * 4 +
+                        ((wv * 2 + p) * 4 + qi) * kStageRow + qq + Q * r;
+      double y = t[0];
+#pragma unroll
+      for (int i = 1; i < 8; ++i) y += t[8 * i];
+      y += dpp_bcast<0xB1>(y);                       // quad_perm [1,0,3,2]
+      if constexpr (L == 4) y += dpp_bcast<0x4E>(y);  // quad_perm [2,3,0,1]
+      const int ks = Q * (g + p) + qq;
+      if (r == 0 && ks < ns && (p == 0 || g + 1 < ng))
+        red[((int64_t)wv * ns + ks) * 4 + qi] = y;
+      __builtin_amdgcn_wave_barrier();
+    }
   }
   __syncthreads();
   for (int idx = tid; idx < ns * 4; idx += kBlock) {
@@ -892,7 +921,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
 
 // Q lanes per wavelength: kBlock / Q wavelengths per block.
 void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStream_t st) {
-  const size_t shm = (size_t)red_rows_per_block(a.red_rows) * a.n_steps * 4 * sizeof(double) +
+  const size_t shm = (size_t)red_lds_doubles(a.red_rows, a.n_steps) * sizeof(double) +
                      (size_t)a.n_steps * sizeof(FastStepS);
   const dim3 grid(nblocks, a.n_atm > 1 ? a.n_atm : 1);
   if (Q == 4) {

@@ -501,8 +501,9 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     bool nan_check = false;
     for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
     const int Q = group_lanes(c);
-    // staged partial sums (mode 2) for the one-lane sweep with two steps in flight
-    if (Q == 1 && depth == 2 && c->red_stage &&
+    // staged partial sums (mode 2): the one-lane sweep with two steps in flight, and the
+    // grouped-lane sweep (two groups in flight)
+    if ((Q > 1 || depth == 2) && c->red_stage &&
         ((size_t)(kBlock / 64) * ns * 4 + (size_t)(kBlock / 64) * 2 * 4 * 72) * sizeof(double) +
                 (size_t)ns * sizeof(FastStepS) <= 48 * 1024)
       f.red_rows = 2;

@@ -432,9 +432,9 @@ def test_species_contraction_matches_per_species_sum(fa, monkeypatch):
         assert_flux_parity(down, od, cond["down"], delta, "F_down " + mode)
 
 
-@pytest.mark.parametrize("red_rows", ["1", "0"])    # per-row or full wave partial sums
+@pytest.mark.parametrize("red_mode", ["stage", "rows", "full"])   # partial-sum layouts
 @pytest.mark.parametrize("n_layers", [34, 36])     # 33 / 35 steps: dummy group slots
-def test_grouped_lane_sweep_matches_one_lane_form(fa, monkeypatch, n_layers, red_rows):
+def test_grouped_lane_sweep_matches_one_lane_form(fa, monkeypatch, n_layers, red_mode):
     """The grouped-lane sweeps (two or four lanes per wavelength, small slices) form every
     flux with the one-lane expressions: one sweep from the same state gives bit-identical
     fluxes and dtaus; only the bolometric partial sums use another fixed summation tree (dT
@@ -449,7 +449,8 @@ def test_grouped_lane_sweep_matches_one_lane_form(fa, monkeypatch, n_layers, red
                                  (Tn / 1000.0) ** 0.5, p, Tn) for n in names}
     mmr = O.mock_mmr(names, M_BAR)[:, None] * np.ones(n_layers)
     out = {}
-    monkeypatch.setenv("FREI_RED_ROWS", red_rows)
+    monkeypatch.setenv("FREI_RED_STAGE", "1" if red_mode == "stage" else "0")
+    monkeypatch.setenv("FREI_RED_ROWS", "1" if red_mode == "rows" else "0")
     for q in (4, 2, 1):
         monkeypatch.setenv("FREI_GROUP_Q", str(q))
         eng = fa.Engine(lam, p, tabs, mmr=mmr)
