@@ -163,8 +163,8 @@ struct frei_ctx {
   int shared_max_blocks = 1024;
   // Grouped-lane sweep (2 or 4 lanes per wavelength): contracted table, LDS step table and
   // at most this many 256-wavelength blocks, i.e. about one wave per SIMD or less.
-  int pair_max_blocks = 640;            // FREI_PAIR_MAX_BLOCKS (<= 164k lambda per GPU)
-  int quad_max_blocks = 128;            // FREI_QUAD_MAX_BLOCKS (<= 32k lambda per GPU)
+  int pair_max_blocks = 420;            // FREI_PAIR_MAX_BLOCKS (<= 107k lambda per GPU)
+  int quad_max_blocks = 208;            // FREI_QUAD_MAX_BLOCKS (<= 53k lambda per GPU)
   int group_q = 0;                      // FREI_GROUP_Q forces 1, 2 or 4 lanes per wavelength
   int red_rows = 1;                     // FREI_RED_ROWS=0: full wave sums per step
   int red_stage = 1;                    // FREI_RED_STAGE=0: no staged sums (one-lane sweep)
