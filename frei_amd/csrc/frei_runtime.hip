@@ -160,7 +160,7 @@ struct frei_ctx {
   // blocks), where each CU runs ~1 block and the per-step scalar loads would miss the K$.
   // FREI_SHARED=0/1 forces it off/on; FREI_SHARED_MAX_BLOCKS moves the threshold.
   int shared_mode = -1;
-  int shared_max_blocks = 420;          // <= 107k lambda (250k: global step table 1 % faster, profiles/r01_shared_sweep.jsonl)
+  int shared_max_blocks = 640;          // <= 164k lambda (125k: LDS 4 % faster; 164k tie; 250k: global 1 % faster)
   // Grouped-lane sweep (2 or 4 lanes per wavelength): contracted table, LDS step table and
   // at most this many 256-wavelength blocks, i.e. about one wave per SIMD or less.
   int pair_max_blocks = 420;            // FREI_PAIR_MAX_BLOCKS (<= 107k lambda per GPU)
