@@ -7,10 +7,13 @@ tables generated on the device.  One step = one radiative-equilibrium T–P iter
 (emit sweep + absorb sweep, each with its bolometric reduction, dT update and the
 convergence test) = 2 × 59 × 500k flux updates, always fully computed (convergence is
 tracked but does not stop the timed work).  With --gpus N the 500k wavelengths are
-sharded over N ranks (strong scaling) with one RCCL all-gather per sweep.
+sharded over N ranks (strong scaling) with one exchange of the per-sweep partial sums (the
+engine's P2P mailboxes over xGMI by default).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
-      (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+      (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...; the
+      launcher only starts the processes: rendezvous, barriers and timing reductions go over
+      plain sockets, the per-sweep exchange is the engine's own)
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -42,9 +45,13 @@ def parse():
     ap.add_argument("--no-binning", action="store_true",
                     help="skip the K6 opacity-binning measurement (rank 0)")
     ap.add_argument("--binning-reps", type=int, default=5)
-    ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
-                    help="N > 1 exchange: RCCL all-gather (default) or the host (gloo) hook; "
-                         "host lets several ranks share one GPU to rehearse the multi-rank flow")
+    ap.add_argument("--comm", choices=("p2p", "rccl", "host"), default="p2p",
+                    help="N > 1 exchange: the engine's P2P mailboxes over xGMI (default; falls "
+                         "back to RCCL if they cannot be set up), RCCL all-gather, or the host "
+                         "hook (lets several ranks share one GPU to rehearse the multi-rank flow)")
+    ap.add_argument("--no-per-species", action="store_true",
+                    help="skip the per-species (no K3 contraction) measurement")
+    ap.add_argument("--per-species-steps", type=int, default=6)
     ap.add_argument("--no-c5", action="store_true",
                     help="skip the batched-atmosphere (C5) measurement")
     ap.add_argument("--c5-lam", type=int, default=100_000)
@@ -53,8 +60,9 @@ def parse():
 
 
 class Dist:
-    """torch.distributed (gloo, CPU only) for rendezvous, barriers and timing reductions;
-    the data-path collective is RCCL inside the native engine."""
+    """Rendezvous, barriers and max-over-ranks timing for one process per GPU, over plain
+    sockets (frei_amd.rendezvous; no PyTorch).  The data-path exchange is the engine's own
+    (P2P mailboxes over xGMI, RCCL or the host hook)."""
 
     def __init__(self, n):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -62,30 +70,23 @@ class Dist:
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         if self.world != n:
             raise SystemExit(f"--gpus {n} but WORLD_SIZE={self.world}")
-        self.dist = None
+        self.rdzv = None
         if self.world > 1:
-            import torch.distributed as dist
-            dist.init_process_group("gloo")   # its notices go to stderr (_reserve_stdout)
-            self.dist = dist
+            from frei_amd.rendezvous import from_env
+            self.rdzv = from_env()
 
     def barrier(self):
-        if self.dist:
-            self.dist.barrier()
+        if self.rdzv:
+            self.rdzv.barrier()
 
     def max(self, x):
-        if not self.dist:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        return self.rdzv.max(x) if self.rdzv else x
 
-    def bcast_bytes(self, b):
-        if not self.dist:
-            return b
-        obj = [b]
-        self.dist.broadcast_object_list(obj, src=0)
-        return obj[0]
+    def all_ok(self, ok):
+        """True when every rank reports ok."""
+        if not self.rdzv:
+            return bool(ok)
+        return all(v == b"1" for v in self.rdzv.all_gather(b"1" if ok else b"0"))
 
 
 def cpu_baseline(w, n_sample, steps=1):
@@ -237,12 +238,49 @@ def _emit_result(line):
     os.write(_RESULT_FD, (json.dumps(line) + "\n").encode())
 
 
+def build_engine(w, tabs, lo, hi, d, kind):
+    """Engine for this rank's slice, joined to the other ranks over ``kind`` (p2p, rccl, host)."""
+    from frei_amd.distributed import host_comm, p2p_comm, rccl_comm
+    from frei_amd.engine import Engine
+    comm = None
+    if d.world > 1:
+        comm = {"p2p": p2p_comm, "rccl": rccl_comm, "host": host_comm}[kind](d.rdzv)
+    return Engine(w["lam"], w["p"], tabs, mmr=w["mmr"], device=d.local, lam_slice=(lo, hi),
+                  comm=comm)
+
+
+def timed_iterations(eng, d, warmup, steps):
+    """Fixed-work T-P iterations: warm-up, then exactly ``steps`` bracketed by a barrier and a
+    stream synchronize on both sides; the max over ranks."""
+    eng.iterate(warmup)
+    eng.synchronize()
+    d.barrier()
+    t0 = time.perf_counter()
+    eng.iterate(steps)
+    eng.synchronize()
+    t1 = time.perf_counter()
+    d.barrier()
+    return d.max(t1 - t0)
+
+
+def sweep_kernel_time(eng, n_iter):
+    """HIP events on the engine's stream around every sweep launch: (avg ms, launches,
+    exchange avg ms, exchange calls)."""
+    eng.timing(True)
+    eng.iterate(n_iter)
+    eng.synchronize()
+    ms, n = eng.timing_read()
+    xms, nx = eng.timing_read_exchange()
+    eng.timing(False)
+    return ms / max(n, 1), n, xms / max(nx, 1), nx
+
+
 def main():
     _reserve_stdout()
     a = parse()
     d = Dist(a.gpus)
     from frei_amd import _native as N
-    from frei_amd.engine import Engine, partition
+    from frei_amd.engine import partition
     from frei_amd.opacity import SeparableTable
     from frei_amd.workloads import bytes_per_update, c3
 
@@ -251,53 +289,46 @@ def main():
     w = c3(n_layers=a.n_layers, n_lam=a.n_lam, n_T=a.n_T)
     nL, n_lam, S = a.n_layers, a.n_lam, len(w["names"])
     lo, hi = partition(n_lam, d.world, d.rank)
-    comm = None
-    if d.world > 1 and a.comm == "host":
-        from frei_amd.distributed import gloo_comm
-        comm = gloo_comm(d.dist, d.world, d.rank)
-    elif d.world > 1:
-        uid = None
-        if d.rank == 0:
-            import ctypes
-            buf = ctypes.create_string_buffer(128)
-            N.check(N.lib().frei_comm_unique_id(buf))
-            uid = buf.raw
-        uid = d.bcast_bytes(uid)
-        comm = ("rccl", d.world, d.rank, uid)
     tabs = {n: SeparableTable(w["base"][s], w["fp"][s], w["fT"][s], w["p"], w["T_nodes"])
             for s, n in enumerate(w["names"])}
-    eng = Engine(w["lam"], w["p"], tabs, mmr=w["mmr"], device=d.local, lam_slice=(lo, hi),
-                 comm=comm)
-    # metadata build + species contraction (K3, once per tables/mmr; outside the timed steps)
+    kind, comm_note = a.comm, None
+    t_e = time.perf_counter()
+    eng, err = None, None
+    try:
+        eng = build_engine(w, tabs, lo, hi, d, kind)
+    except RuntimeError as e:   # e.g. no IPC / peer mapping: fall back to RCCL everywhere
+        err = str(e)
+    if not d.all_ok(eng is not None):
+        if kind != "p2p":
+            raise SystemExit(f"rank {d.rank}: engine setup failed: {err}")
+        if eng is not None:
+            eng.close()
+        comm_note = f"p2p setup failed ({err or 'on a peer rank'}); fell back to RCCL"
+        kind = "rccl"
+        eng = build_engine(w, tabs, lo, hi, d, kind)
+    tables_s = time.perf_counter() - t_e
+    # one-time setup: metadata build + species contraction (K3), outside the timed steps
     t_s = time.perf_counter()
     path = eng.path()
     setup_ms = (time.perf_counter() - t_s) * 1e3
+    setup_phases = eng.setup_timing()
 
-    # ---- timed fixed-work T-P iterations (no per-kernel events inside the timed region)
+    # ---- headline: timed fixed-work T-P iterations (no per-kernel events inside)
     eng.state_init(w["T0"])
-    eng.iterate(a.warmup)
-    eng.synchronize()
-    d.barrier()
-    t0 = time.perf_counter()
-    eng.iterate(a.steps)
-    eng.synchronize()
-    t1 = time.perf_counter()
-    d.barrier()
-    elapsed = d.max(t1 - t0)
+    elapsed = timed_iterations(eng, d, a.warmup, a.steps)
     # ---- sweep-kernel duration: HIP events on the engine's stream around every sweep launch
-    eng.timing(True)
-    eng.iterate(max(2, a.steps // 2))
-    eng.synchronize()
-    sweep_ms, n_sweeps = eng.timing_read()
-    xch_ms, n_xch = eng.timing_read_exchange()
-    eng.timing(False)
+    avg_sweep_ms, n_sweeps, xch_ms, n_xch = sweep_kernel_time(eng, max(2, a.steps // 2))
     exchange = None
-    if d.world > 1:   # per-sweep rank exchange (HIP events on the engine stream), max over ranks
-        exchange = {"kind": ("RCCL all-gather" if a.comm == "rccl" else "host all-gather")
-                            + f" of {4 * (nL - 1) * 8} B per rank",
-                    "avg_ms": d.max(xch_ms / max(n_xch, 1)), "calls": n_xch,
-                    "note": "stream time from the start of the exchange to the end of the "
-                            "all-gather, per sweep (includes waiting for the slowest rank)"}
+    if d.world > 1:   # per-sweep rank exchange, max over ranks
+        what = {"p2p": "P2P mailbox push over xGMI (update-kernel wait)",
+                "rccl": "RCCL all-gather", "host": "host all-gather"}[kind]
+        exchange = {"kind": f"{what} of {4 * (nL - 1) * 8} B per rank",
+                    "avg_ms": d.max(xch_ms), "calls": n_xch,
+                    "note": comm_note or ("P2P: time the update kernel waits for every rank's "
+                                          "sums (includes the slowest rank's lag)"
+                                          if kind == "p2p" else
+                                          "stream time of the all-gather, per sweep "
+                                          "(includes waiting for the slowest rank)")}
     updates_per_step = 2 * (nL - 1) * n_lam
     value = updates_per_step * a.steps / elapsed
     ms_per_step = elapsed / a.steps * 1e3
@@ -305,15 +336,16 @@ def main():
     # ---- roofline of the dominant kernel (sweep), per launch, this rank's slice
     S_run = 1 if path["contracted"] else S    # K3 sweeps read one contracted table
     bpu = bytes_per_update(S_run, live_only=True)
-    avg_sweep_s = (sweep_ms / max(n_sweeps, 1)) * 1e-3
     bytes_launch = bpu * (nL - 1) * (hi - lo)
-    achieved = bytes_launch / avg_sweep_s
+    achieved = bytes_launch / (avg_sweep_ms * 1e-3)
     achieved = d.max(achieved) if d.world > 1 else achieved
 
-    # ---- iterations to radiative equilibrium (reference convergence test); one untimed run
-    # first so the one-time buffers (T history, the final emit's dtaus) are allocated
+    # ---- iterations to radiative equilibrium (reference convergence test); the first run
+    # allocates the one-time buffers (T history, the final emit's dtaus)
+    t_c = time.perf_counter()
     eng.run(w["T0"], n_timesteps=a.rad_eq_max, n_zero_crossings=2, convergence_dT=3.0,
             alpha=1.0, want_dtaus=False)
+    cold_s = time.perf_counter() - t_c
     d.barrier()
     t2 = time.perf_counter()
     out = eng.run(w["T0"], n_timesteps=a.rad_eq_max, n_zero_crossings=2, convergence_dT=3.0,
@@ -322,30 +354,52 @@ def main():
     rad_eq_wall = d.max(t3 - t2)
     n_iter = out["n_iter"]
 
-    # PMC traffic of the same workload (separate rocprofv3 --pmc passes, committed)
-    traffic, traffic_src = None, None
+    # ---- per-species path (no K3): the sweep sums all S species' table rows per step, the
+    # form any T-dependent chemistry needs; same workload, fixed work
+    per_species = None
+    if not a.no_per_species:
+        eng.set_option("precontract", 0)
+        p2 = eng.path()
+        eng.state_init(w["T0"])
+        el_ps = timed_iterations(eng, d, 2, a.per_species_steps)
+        ps_ms, ps_n, _, _ = sweep_kernel_time(eng, a.per_species_steps)
+        bpu_ps = bytes_per_update(S, live_only=True)
+        ach_ps = d.max(bpu_ps * (nL - 1) * (hi - lo) / (ps_ms * 1e-3))
+        per_species = {
+            "value": updates_per_step * a.per_species_steps / el_ps, "unit": "updates/s",
+            "ms_per_step": el_ps / a.per_species_steps * 1e3, "steps": a.per_species_steps,
+            "path": p2,
+            "roofline": {"bound": "hbm", "achieved": ach_ps / 1e9, "peak": PEAK_HBM / 1e9,
+                         "unit": "GB/s", "frac": ach_ps / PEAK_HBM, "kernel": "sweep_fast_kernel",
+                         "bytes_per_update": bpu_ps, "avg_launch_ms": ps_ms, "launches": ps_n},
+            "byte_model": f"8 stale opposite-stream read + 8 live flux write + 16*S = {bpu_ps} B "
+                          f"(SURVEY 8(d)'s 24 + 16*S = {24 + 16 * S} B less the dead store the "
+                          "T-P loop skips)"}
+        eng.set_option("precontract", -1)
+        eng.path()
+    cpu = None
+    if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
+        rate, dt = cpu_baseline(w, min(a.cpu_lam, n_lam))
+        cpu = {"value": rate, "unit": "updates/s", "cores": 1, "host_cpus": os.cpu_count(),
+               "kind": "port",
+               "sample": f"oracle (NumPy restatement of frei's path, single-threaded: 1 of "
+                         f"{os.cpu_count()} host CPUs), {nL} layers x {min(a.cpu_lam, n_lam)} "
+                         f"lambda (evenly strided sample of the same grid), {S} species, 1 T-P "
+                         f"iteration + final emit, {dt:.1f} s"}
+    eng.close()
+
+    # PMC traffic / VALU of the same workload (separate rocprofv3 --pmc passes, committed)
+    traffic, traffic_src, valu = None, None, None
     tpath = os.path.join(ROOT, "profiles", "traffic_sweep.json")
     if os.path.exists(tpath):
         t = json.load(open(tpath))
         if t["workload"] == {"n_lam": n_lam // d.world, "n_layers": nL, "species": S,
                              "contracted": path["contracted"]}:
             traffic, traffic_src = t, "profiles/traffic_sweep.json"
-
-    # VALU utilisation of the same workload (rocprofv3 SQ counters, committed): the sweep
-    # moved from HBM-bound to fp64-VALU-bound once it reads one contracted table (K3)
-    valu = None
     vpath = os.path.join(ROOT, "profiles", "valu_sweep.json")
     if os.path.exists(vpath) and traffic is not None:
         valu = json.load(open(vpath))
 
-    cpu = None
-    if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
-        rate, dt = cpu_baseline(w, min(a.cpu_lam, n_lam))
-        cpu = {"value": rate, "unit": "updates/s", "cores": 1, "kind": "port",
-               "sample": f"oracle (NumPy restatement of frei's path), {nL} layers x "
-                         f"{min(a.cpu_lam, n_lam)} lambda (evenly strided sample of the same "
-                         f"grid), {S} species, 1 T-P iteration + final emit, {dt:.1f} s"}
-    eng.close()
     c5 = None if a.no_c5 else c5_leg(a, d)
     binning = None
     if d.rank == 0 and not a.no_binning:
@@ -368,16 +422,24 @@ def main():
                                    f"(H2O/CO/CO2/CH4/Na/K + H2-H2/H2-He CIA), {a.n_T} T-nodes, "
                                    "1 step = 1 T-P iteration (emit+absorb)",
                        "n_layers": nL, "n_lambda": n_lam, "n_species": S, "n_T": a.n_T,
-                       "parallelism": f"lambda-shard x{d.world} "
-                                      + ("(RCCL all-gather per sweep)" if a.comm == "rccl"
-                                         else "(host all-gather per sweep, rehearsal)")},
+                       "parallelism": f"lambda-shard x{d.world}"
+                                      + ("" if d.world == 1 else f" ({kind} exchange per sweep)")},
             "tp_iters_per_s": 1e3 / ms_per_step,
             "exchange": exchange,
-            "sweep_path": dict(path, setup_ms=setup_ms,
+            "sweep_path": dict(path, setup_ms=setup_ms, setup_phases_ms=setup_phases,
+                               tables_s=tables_s,
                                note="setup_ms: one-time metadata build + species contraction "
-                                    "(K3) per tables/mmr, outside the timed steps"),
+                                    "(K3) per tables/mmr, outside the timed steps; tables_s: "
+                                    "context creation + device table generation"),
             "rad_eq": {"iterations": n_iter, "max_iterations": a.rad_eq_max,
-                       "wall_s": rad_eq_wall, "iters_per_s": n_iter / rad_eq_wall},
+                       "wall_s": rad_eq_wall, "iters_per_s": n_iter / rad_eq_wall,
+                       "setup_s": setup_ms * 1e-3,
+                       "wall_incl_setup_s": rad_eq_wall + setup_ms * 1e-3,
+                       "iters_per_s_incl_setup": n_iter / (rad_eq_wall + setup_ms * 1e-3),
+                       "first_run_s": cold_s,
+                       "note": "wall_s: warm run (T-P iterations to convergence + final emit); "
+                               "first_run_s: the first run, with its one-time buffer "
+                               "allocations"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM,
                          "traffic": traffic["hbm_B_per_launch"] if traffic else None,
@@ -392,7 +454,19 @@ def main():
                          if valu else None,
                          "kernel": "sweep_fast_kernel", "bytes_per_update": bpu,
                          "bytes_per_launch": bytes_launch,
-                         "avg_launch_ms": avg_sweep_s * 1e3, "launches": n_sweeps},
+                         "avg_launch_ms": avg_sweep_ms, "launches": n_sweeps,
+                         "byte_model": (f"contracted table (K3): 8 stale opposite-stream read + "
+                                        f"8 live flux write + 16 (two rows of one table) = {bpu} B"
+                                        if path["contracted"] else
+                                        f"8 + 8 + 16*S = {bpu} B"),
+                         "survey_byte_model_equivalent": {
+                             "bytes_per_update": 24 + 16 * S,
+                             "effective_GBps": value / d.world * (24 + 16 * S) / 1e9,
+                             "note": "value x SURVEY 8(d)'s (24 + 16 S) B: the traffic the "
+                                     "reference's per-species assembly would need; above the "
+                                     "HBM peak because K3 hoists the species sum out of the "
+                                     "loop"}},
+            "per_species": per_species,
             "cpu_baseline": cpu,
             "k6_binning": binning,
             "c5_batched": c5,

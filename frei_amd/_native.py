@@ -34,6 +34,7 @@ SIGNATURES = {
     "frei_ctx_create_batch": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int,
                                              _i64, ctypes.c_int, ctypes.c_int]),
     "frei_set_gravity": (ctypes.c_int, [_vp, _dp]),
+    "frei_set_ftoa_batch": (ctypes.c_int, [_vp, _dp]),
     "frei_run_batch": (ctypes.c_int, [_vp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                       ctypes.c_double, _ip, _dp, _dp]),
     "frei_set_grid": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, ctypes.c_double,
@@ -58,14 +59,18 @@ SIGNATURES = {
     "frei_kappa": (ctypes.c_int, [_vp, ctypes.c_double, ctypes.c_double, _dp, _dp]),
     "frei_propagate_fluxes": (ctypes.c_int, [ctypes.c_int, _i64, _dp, _dp, _dp, _dp,
                                              ctypes.c_double, ctypes.c_double, _dp, _dp, _dp,
-                                             _dp]),
+                                             _dp, _dp]),
     "frei_comm_unique_id": (ctypes.c_int, [_vp]),
     "frei_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp]),
+    "frei_comm_p2p_handle": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp]),
+    "frei_comm_p2p_open": (ctypes.c_int, [_vp, _vp]),
     "frei_comm_init_host": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
                                            "ALLGATHER_FN", _vp]),
     "frei_ctx_path": (ctypes.c_int, [_vp, _ip]),
     "frei_milne_pressure": (ctypes.c_int, [_vp, _dp, _dp, _dp]),
     "frei_contribution": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, ctypes.c_double, _dp]),
+    "frei_set_option": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int]),
+    "frei_setup_timing": (ctypes.c_int, [_vp, _dp]),
     "frei_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "frei_timing_read": (ctypes.c_int, [_vp, _dp, _ip]),
     "frei_timing_read_exchange": (ctypes.c_int, [_vp, _dp, _ip]),

@@ -24,8 +24,9 @@ __all__ = ["BatchEngine", "batched_emission_spectra"]
 
 class BatchEngine:
     """``n_atm`` atmospheres on ``device``: ``g`` [n_atm] (cm s^-2), ``mmr``
-    [n_atm][n_species][n_layers]; wavelengths, pressures (bar, descending), opacities, m_bar
-    and F_TOA are shared (as in a grid of Planets that differ in T, g and metallicity)."""
+    [n_atm][n_species][n_layers], ``F_toa`` [n_lam] shared or [n_atm][n_lam] per atmosphere;
+    wavelengths, pressures (bar, descending), opacities and m_bar are shared (as in a grid of
+    Planets that differ in T, g, metallicity and irradiation)."""
 
     def __init__(self, lam_um, p_bar, opacities, g, mmr=None, m_bar=M_BAR_DEFAULT, F_toa=None,
                  device=0):
@@ -44,6 +45,10 @@ class BatchEngine:
         lk = N.f64(lam_cm * K_B)
         sig = N.f64(sigma_scattering(self.lam_um, self.m_bar))
         ft = N.f64(f_toa(self.lam_um) if F_toa is None else value(F_toa, "erg / (s cm3)"))
+        ft_atm = None
+        if ft.ndim == 2:     # one F_TOA per atmosphere (planets around different stars)
+            ft_atm = N.f64(np.broadcast_to(ft, (self.n_atm, self.n_lam)))
+            ft = N.f64(ft_atm[0])
         wtr = N.f64(trapz_weights(lam_cm))
         p_cgs = N.f64(self.p_bar * BAR)
         ctx = ctypes.c_void_p()
@@ -54,6 +59,8 @@ class BatchEngine:
                                   N.dptr(wtr), N.dptr(p_cgs), float(self.g[0]), self.m_bar))
         if self.n_atm > 1:
             N.check(lib.frei_set_gravity(ctx, N.dptr(self.g)))
+            if ft_atm is not None:
+                N.check(lib.frei_set_ftoa_batch(ctx, N.dptr(ft_atm)))
         self.lo = 0  # the whole wavelength grid
         # tables: the single-atmosphere engine's upload paths (shared by every atmosphere)
         for s, name in enumerate(self.names):
@@ -144,9 +151,13 @@ def batched_emission_spectra(grids, n_timesteps=1, n_zero_crossings=2, convergen
                            m_bar=gr.planet.m_bar)
             mmrs.append(np.array([mm[n] for n in names]))
     pl = g0.planet
+    # each planet's own irradiation (core.py:262): one F_TOA per atmosphere when they differ
+    ft = np.array([F_TOA(g0.lam, T_star=gr.planet.T_star, a_rstar=gr.planet.a_rstar)
+                   for gr in grids])
+    if all(np.array_equal(f, ft[0]) for f in ft[1:]):
+        ft = ft[0]
     eng = BatchEngine(g0.lam, g0.pressures, g0.opacities, [gr.planet.g for gr in grids],
-                      mmr=np.array(mmrs), m_bar=pl.m_bar,
-                      F_toa=F_TOA(g0.lam, T_star=pl.T_star, a_rstar=pl.a_rstar), device=device)
+                      mmr=np.array(mmrs), m_bar=pl.m_bar, F_toa=ft, device=device)
     try:
         out = eng.run(np.array([gr.init_temperatures for gr in grids]), n_timesteps,
                       n_zero_crossings, scalar(convergence_dT, "K"), pl.alpha)

@@ -1,4 +1,5 @@
 """Build libfrei_hip.so in-tree for gfx950:  python -m frei_amd.build"""
+import glob
 import os
 import subprocess
 import sys
@@ -12,8 +13,9 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-shared"
 def build(verbose=False):
     out = os.path.join(HERE, "libfrei_hip.so")
     srcs = [os.path.join(HERE, s) for s in SOURCES]
-    deps = srcs + [os.path.join(HERE, "csrc", "frei_device.h"),
-                   os.path.join(ROOT, "include", "frei_hip.h")]
+    # every header the sources include (frei_math.h holds the sweep's division/sqrt cores)
+    deps = (srcs + sorted(glob.glob(os.path.join(HERE, "csrc", "*.h"))) +
+            sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
     if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -125,6 +125,7 @@ class Grid:
         if self._engine is not None:
             self._engine.close()
             self._engine = None
+        self._last_dtaus = None   # its device copy went with the engine
 
     def engine(self):
         if self._engine is None:

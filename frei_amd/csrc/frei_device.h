@@ -179,6 +179,7 @@ struct AtmStride {
   int64_t flux;      // F_up / F_down / dtaus [n_layers][n_lam]
   int64_t tab;       // contracted opacity table
   int64_t part;      // block partial sums [n_steps * 4][blocks]
+  int64_t ftoa;      // per-atmosphere F_TOA [n_lam] (0: one F_TOA shared by all)
   const double* g;   // per-atmosphere gravity (nullptr: SetupArgs.g)
 };
 
@@ -234,8 +235,41 @@ struct SweepArgs {
   const int* conv;
 };
 
+// P2P exchange of the per-sweep bolometric partial sums over xGMI, no RCCL and no host in the
+// loop.  Every rank owns a mailbox in uncached device memory that every other
+// rank has mapped through an IPC handle; per sweep each rank's reduce kernel pushes its n sums
+// into slot [rank] of every mailbox, then a sequence flag per value; the update kernel polls
+// its own mailbox until every rank's flags carry the sweep's sequence number and sums the
+// ranks in rank order.  Two parity slots: a rank can run at most one sweep ahead of another
+// (its next update needs everyone's next sums), so slot seq & 1 is never overwritten while a
+// slower rank still reads it.
+struct P2PPush {
+  double* const* peers;    // [nranks] every rank's mailbox (own included), device pointers
+  int nranks, rank;
+  int64_t n;               // sums per rank (n_steps * 4)
+  uint64_t seq;            // this sweep's sequence number (> 0); nullptr peers: no push
+};
+struct P2PWait {
+  const double* mbox;      // this rank's mailbox (nullptr: no P2P exchange)
+  int nranks;
+  int64_t n;
+  uint64_t seq;
+  int64_t timeout_ticks;   // wall_clock64 ticks before a missing peer is reported
+  int* err;                // set to 1 when a peer never published (timeout)
+  unsigned long long* wait_ticks;  // accumulated ticks thread 0 spent waiting (diagnostic)
+};
+// mailbox layout: values [2][nranks][n] doubles, then flags [2][nranks][n] uint64
+__host__ __device__ inline int64_t mbox_val(int par, int r, int R, int64_t n) {
+  return ((int64_t)par * R + r) * n;
+}
+__host__ __device__ inline int64_t mbox_flag(int par, int r, int R, int64_t n) {
+  return 2 * (int64_t)R * n + ((int64_t)par * R + r) * n;
+}
+__host__ __device__ inline size_t mbox_bytes(int R, int64_t n) { return (size_t)4 * R * n * 8; }
+
 struct UpdateArgs {
   SetupArgs su;
+  P2PWait p2p;
   int dir, next_dir, nranks, force, track, stop_on_conv, n_zero_crossings, hist_cap;
   int meta_in_lds;         // per-(species, layer) metadata staged in LDS (small grids)
   double m_bar, alpha, convergence_dT;
@@ -249,6 +283,16 @@ struct UpdateArgs {
   int* conv;
 };
 
+// LDS bytes of the update kernel (K4/K5): T, dT, p, T before/after absorb, ln p ratios,
+// sorted T nodes, rank-summed partials, 3 int state arrays; then (meta) the per-(species,
+// layer) pressure brackets and mixing ratios and the species metadata.
+__host__ __device__ inline size_t update_lds_bytes(int nL, int ntn, int S, bool meta) {
+  size_t b = (size_t)(8 * nL + ntn + 4 * (nL - 1)) * sizeof(double) + 3 * (size_t)nL * sizeof(int);
+  b = (b + 15) & ~(size_t)15;
+  if (meta) b += (size_t)S * nL * (sizeof(PMeta) + sizeof(double)) + (size_t)S * sizeof(SpecMeta);
+  return b;
+}
+
 // launchers (frei_kernels.hip)
 void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st);
 void launch_sweep_fast(int dir, int S, int depth, bool nan_check, bool shared,
@@ -259,13 +303,17 @@ void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStrea
 void launch_nan_scan(const double* x, int64_t n, int* flag, hipStream_t st);
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
                    int force, hipStream_t st, int n_atm = 1, int64_t part_stride = 0,
-                   int64_t fb_stride = 0);
+                   int64_t fb_stride = 0, const P2PPush* push = nullptr);
+// One tiny launch that publishes flag value `seq` for this rank in every mailbox and waits
+// for every rank's (the P2P handshake at communicator setup).
+void launch_p2p_handshake(const P2PPush& push, const P2PWait& wait, hipStream_t st);
 void launch_setup(const SetupArgs& u, int dir, hipStream_t st, int n_atm = 1);
 void launch_log_ratio(const double* p, double p_top2, int nL, double* lnp, hipStream_t st);
 void launch_update(const UpdateArgs& a, hipStream_t st, int n_atm = 1);
 void launch_propagate(int64_t n, const double* c1, const double* lk, const double* F1u,
                       const double* F2d, double T1, double T2, const double* dtau,
-                      const double* w0, double* F2u, double* F1d, hipStream_t st);
+                      const double* w0, const double* g0, double* F2u, double* F1d,
+                      hipStream_t st);
 void launch_kappa(int64_t n, const TermP* terms, int nS, const double* sig, double* k,
                   hipStream_t st);
 void launch_gen_table(double* tab, const double* base, const double* fp, const double* fT,

@@ -84,6 +84,36 @@ __device__ __forceinline__ void two_stream(double w0, double dtau, double B1, do
               pi_w * ((B1 * (chi + xi) - psi * B2) + q * ((xi + psi) - chi)));
 }
 
+// propagate_fluxes with an asymmetry factor g0 (twostream.py:139-176, E of :89-94), the
+// reference's numpy expression order term by term; IEEE operations throughout (standalone
+// API only: E - w0 may be <= 0 for strongly back-scattering g0, giving NaN as numpy does).
+__device__ __forceinline__ void two_stream_g(double w0, double g0, double dtau, double B1,
+                                             double B2, double F1u, double F2d, double& F2u,
+                                             double& F1d) {
+  const double E = (w0 > 0.1) ? (((((1.225 - 0.1582 * g0) - 0.1777 * w0) - 0.07465 * (g0 * g0)) +
+                                  (0.2351 * w0) * g0) - 0.05582 * (w0 * w0))
+                              : 1.0;
+  const double Emw = E - w0;
+  const double wg = 1.0 - w0 * g0;
+  const double Tr = ::exp((-2.0 * ::sqrt((E * Emw) * wg)) * dtau);
+  const double r = ::sqrt((Emw / E) / wg);
+  const double zp = 0.5 * (1.0 + r);
+  const double zm = 0.5 * (1.0 - r);
+  const double Tr2 = Tr * Tr;
+  const double zm2 = zm * zm;
+  const double zp2 = zp * zp;
+  const double chi = zm2 * Tr2 - zp2;
+  const double xi = (zp * zm) * (1.0 - Tr2);
+  const double psi = (zm2 - zp2) * Tr;
+  const double pi_w = (kPi * (1.0 - w0)) / Emw;
+  const double q = ((B1 - B2) / dtau) / ((2.0 * E) * wg);
+  const double ic = 1.0 / chi;
+  F2u = ic * ((psi * F1u - xi * F2d) +
+              pi_w * ((B2 * (chi + xi) - psi * B1) + q * ((chi - psi) - xi)));
+  F1d = ic * ((psi * F2d - xi * F1u) +
+              pi_w * ((B1 * (chi + xi) - psi * B2) + q * ((xi + psi) - chi)));
+}
+
 // Species-summed opacity at one wavelength (opacity.py:250-269).  FAST: every term is
 // exactly two T-bracket rows of the layer's own pressure slab (pressure on a node).
 template <int S, bool FAST>
@@ -411,6 +441,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     st += m * a.bs.steps;
     ss += m * a.bs.steps;
     a.tab[0] += m * a.bs.tab;
+    a.ftoa += m * a.bs.ftoa;
     a.conv += m;
   }
   if (!a.force && *a.conv) return;
@@ -685,6 +716,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     if (dtaus) dtaus += m * a.bs.flux;
     ss += m * a.bs.steps;
     a.tab[0] += m * a.bs.tab;
+    a.ftoa += m * a.bs.ftoa;
     a.conv += m;
   }
   if (!a.force && *a.conv) return;
@@ -942,11 +974,69 @@ void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStrea
 }
 
 
+// ---------------------------------------------------------------- P2P exchange
+// System-scope stores of a value and then its flag into every rank's mailbox (P2PPush): the
+// release fence orders the value stores before the flag stores for any observer; the
+// explicit wait keeps the compiler from dropping the fence's completion wait (gfx950 hazard,
+// MI355X_MICROARCH.md "Compiler hazard").
+__device__ __forceinline__ void p2p_push_values(const P2PPush& p, int64_t idx, const double* v,
+                                                int nv) {
+  const int par = (int)(p.seq & 1);
+  for (int r = 0; r < p.nranks; ++r) {
+    uint64_t* dst = reinterpret_cast<uint64_t*>(p.peers[r] + mbox_val(par, p.rank, p.nranks, p.n));
+    for (int k = 0; k < nv; ++k)
+      __hip_atomic_store(dst + idx + k, __builtin_bit_cast(uint64_t, v[k]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int r = 0; r < p.nranks; ++r) {
+    uint64_t* fl = reinterpret_cast<uint64_t*>(p.peers[r]) + mbox_flag(par, p.rank, p.nranks, p.n);
+    for (int k = 0; k < nv; ++k)
+      __hip_atomic_store(fl + idx + k, p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Wait until rank r's value idx of this sweep is published (flag == seq) or the timeout
+// passes (then *err = 1 and the value is used as is: the run is reported failed, not hung).
+__device__ __forceinline__ double p2p_take(const P2PWait& w, int r, int64_t idx,
+                                           long long t0) {
+  const int par = (int)(w.seq & 1);
+  const uint64_t* fl =
+      reinterpret_cast<const uint64_t*>(w.mbox) + mbox_flag(par, r, w.nranks, w.n) + idx;
+  while (__hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != w.seq) {
+    if (wall_clock64() - t0 > w.timeout_ticks) {
+      __hip_atomic_store(w.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  // the mailbox is uncached and this load bypasses the caches: it is issued only after the
+  // flag load returned the new sequence number, behind the producer's release
+  const uint64_t* vp =
+      reinterpret_cast<const uint64_t*>(w.mbox + mbox_val(par, r, w.nranks, w.n)) + idx;
+  return __builtin_bit_cast(double,
+                            __hip_atomic_load(vp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
+__global__ void p2p_handshake_kernel(P2PPush push, P2PWait wait) {
+  if (threadIdx.x != 0) return;
+  const double one = 1.0;
+  p2p_push_values(push, 0, &one, 1);
+  const long long t0 = wall_clock64();
+  for (int r = 0; r < wait.nranks; ++r) (void)p2p_take(wait, r, 0, t0);
+}
+
+void launch_p2p_handshake(const P2PPush& push, const P2PWait& wait, hipStream_t st) {
+  hipLaunchKernelGGL(p2p_handshake_kernel, dim3(1), dim3(64), 0, st, push, wait);
+}
+
 // ---------------------------------------------------------------- partial sums
 __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ part,
                                                      int nblocks, double* __restrict__ Fb,
                                                      const int* conv, int force,
-                                                     int64_t part_stride, int64_t fb_stride) {
+                                                     int64_t part_stride, int64_t fb_stride,
+                                                     P2PPush push) {
   part += blockIdx.y * part_stride;   // atmosphere of a batched launch
   Fb += blockIdx.y * fb_stride;
   conv += blockIdx.y;
@@ -959,7 +1049,11 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) Fb[blockIdx.x] = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+  if (threadIdx.x == 0) {
+    const double v = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+    if (push.peers) p2p_push_values(push, blockIdx.x, &v, 1);
+    else Fb[blockIdx.x] = v;
+  }
 }
 
 // ln(p_l / p_{l+1}) per layer, the top entry with emit's extrapolated p_2 (twostream.py:
@@ -1122,12 +1216,6 @@ __device__ double layer_dT(const double* Fb, double T1, double T2, double p1, do
 // T nodes, the all-gathered partial sums, the T-P history state and — when it fits — the
 // per-(species, layer) interpolation metadata) into LDS; the dT physics, the convergence
 // bookkeeping and the next sweep's bracket searches then run from LDS.
-__host__ __device__ inline size_t update_lds_bytes(int nL, int ntn, int S, bool meta) {
-  size_t b = (size_t)(8 * nL + ntn + 4 * (nL - 1)) * sizeof(double) + 3 * (size_t)nL * sizeof(int);
-  b = (b + 15) & ~(size_t)15;
-  if (meta) b += (size_t)S * nL * (sizeof(PMeta) + sizeof(double)) + (size_t)S * sizeof(SpecMeta);
-  return b;
-}
 
 __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
   atm_view(a, blockIdx.x);  // identity for one atmosphere
@@ -1171,10 +1259,22 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
     }
   }
   for (int q = threadIdx.x; q < ntn; q += blockDim.x) sTn[q] = a.su.tnodes[q];
-  for (int q = threadIdx.x; q < ns * 4; q += blockDim.x) {
-    double v = a.Fb[q];
-    for (int r = 1; r < a.nranks; ++r) v += a.Fb[(int64_t)r * ns * 4 + q];  // rank order
-    sFb[q] = v;
+  if (a.p2p.mbox) {   // P2P: wait for every rank's sums of this sweep, add in rank order
+    const long long t0 = wall_clock64();
+    for (int q = threadIdx.x; q < ns * 4; q += blockDim.x) {
+      double v = p2p_take(a.p2p, 0, q, t0);
+      for (int r = 1; r < a.p2p.nranks; ++r) v += p2p_take(a.p2p, r, q, t0);
+      sFb[q] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && a.p2p.wait_ticks)
+      atomicAdd(a.p2p.wait_ticks, (unsigned long long)(wall_clock64() - t0));
+  } else {
+    for (int q = threadIdx.x; q < ns * 4; q += blockDim.x) {
+      double v = a.Fb[q];
+      for (int r = 1; r < a.nranks; ++r) v += a.Fb[(int64_t)r * ns * 4 + q];  // rank order
+      sFb[q] = v;
+    }
   }
   if (meta) {
     for (int q = threadIdx.x; q < S * nL; q += blockDim.x) {
@@ -1252,13 +1352,16 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
 // ---------------------------------------------------------------- standalone kernels
 __global__ void propagate_kernel(int64_t n, const double* c1, const double* lk,
                                  const double* F1u, const double* F2d, double T1, double T2,
-                                 const double* dtau, const double* w0, double* F2u,
-                                 double* F1d) {
+                                 const double* dtau, const double* w0, const double* g0,
+                                 double* F2u, double* F1d) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   double u, d;
-  two_stream(w0[j], dtau[j], planck(c1[j], lk[j], T1), planck(c1[j], lk[j], T2), F1u[j],
-             F2d[j], u, d);
+  const double B1 = planck(c1[j], lk[j], T1), B2 = planck(c1[j], lk[j], T2);
+  if (g0)
+    two_stream_g(w0[j], g0[j], dtau[j], B1, B2, F1u[j], F2d[j], u, d);
+  else
+    two_stream(w0[j], dtau[j], B1, B2, F1u[j], F2d[j], u, d);
   F2u[j] = u;
   F1d[j] = d;
 }
@@ -1593,9 +1696,11 @@ void launch_nan_scan(const double* x, int64_t n, int* flag, hipStream_t st) {
 
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
                    int force, hipStream_t st, int n_atm, int64_t part_stride,
-                   int64_t fb_stride) {
+                   int64_t fb_stride, const P2PPush* push) {
+  P2PPush p{};
+  if (push) p = *push;
   hipLaunchKernelGGL(reduce_kernel, dim3(n_idx, n_atm), dim3(256), 0, st, part, nblocks, Fb,
-                     conv, force, part_stride, fb_stride);
+                     conv, force, part_stride, fb_stride, p);
 }
 
 void launch_setup(const SetupArgs& u, int dir, hipStream_t st, int n_atm) {
@@ -1610,10 +1715,11 @@ void launch_update(const UpdateArgs& a, hipStream_t st, int n_atm) {
 
 void launch_propagate(int64_t n, const double* c1, const double* lk, const double* F1u,
                       const double* F2d, double T1, double T2, const double* dtau,
-                      const double* w0, double* F2u, double* F1d, hipStream_t st) {
+                      const double* w0, const double* g0, double* F2u, double* F1d,
+                      hipStream_t st) {
   const int nb = (int)((n + 255) / 256);
   hipLaunchKernelGGL(propagate_kernel, dim3(nb), dim3(256), 0, st, n, c1, lk, F1u, F2d, T1,
-                     T2, dtau, w0, F2u, F1d);
+                     T2, dtau, w0, g0, F2u, F1d);
 }
 
 void launch_kappa(int64_t n, const TermP* terms, int nS, const double* sig, double* k,

@@ -5,6 +5,8 @@
 // (one ncclAllGather of n_layers*4 doubles per sweep).
 #include <dlfcn.h>
 
+#include <cctype>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -169,6 +171,18 @@ struct frei_ctx {
   int red_rows = 1;                     // FREI_RED_ROWS=0: full wave sums per step
   int red_stage = 1;                    // FREI_RED_STAGE=0: no staged sums (one-lane sweep)
   int depth4_max_blocks = 0;            // FREI_DEPTH4_MAX_BLOCKS (4 steps in flight: off, measured no faster)
+  size_t lds_per_block = 64 * 1024;     // hipDeviceProp sharedMemPerBlock
+  bool ftoa_per_atm = false;            // batched: one F_TOA per atmosphere (frei_set_ftoa_batch)
+  double setup_ms[5] = {0, 0, 0, 0, 0};  // last metadata build, by phase (frei_setup_timing)
+  // P2P exchange over xGMI (frei_comm_p2p_*): own mailbox (uncached device memory), the
+  // mapped mailboxes of every rank (own included) and the per-sweep sequence number
+  double* d_mbox = nullptr;
+  double** d_peers = nullptr;
+  std::vector<void*> peer_mapped;        // IPC mappings to close
+  uint64_t p2p_seq = 0;
+  int* d_comm_err = nullptr;             // set by a kernel when a peer never published
+  unsigned long long* d_wait_ticks = nullptr;
+  double p2p_timeout_s = 30.0;           // FREI_P2P_TIMEOUT_S
   frei_allgather_fn host_ag = nullptr;  // host all-gather callback (alternative to RCCL)
   void* host_ag_user = nullptr;
   double* h_ag = nullptr;               // pinned [nranks + 1][n_steps * 4]
@@ -208,7 +222,8 @@ int h2d(T* d, const T* h, size_t n, hipStream_t st) {
 
 // Species contraction (K3) when every species shares its nodes (one bracket per layer), no
 // table holds a NaN (the reference's nansum, Q8, is per species) and S >= 2.
-int build_contracted(frei_ctx* c, bool shared_fast) {
+template <typename Lap>
+int build_contracted(frei_ctx* c, bool shared_fast, Lap&& lap) {
   const int nL = c->nL, S = c->S;
   const bool batch = c->n_atm > 1;
   bool on = shared_fast && (S >= 2 || batch) && (c->eff_mode != 0 || batch);
@@ -243,8 +258,10 @@ int build_contracted(frei_ctx* c, bool shared_fast) {
     TRY(dalloc(&c->d_eff, need));
     c->eff_cap = need;
   }
+  lap(2);
   c->eff_stride = per;
   HIP_TRY(hipMemsetAsync(c->d_eff, 0, need * sizeof(double), c->stream));
+  lap(3);
   if (!c->d_ones) {
     std::vector<double> ones(nL, 1.0);
     TRY(dalloc(&c->d_ones, nL));
@@ -261,6 +278,7 @@ int build_contracted(frei_ctx* c, bool shared_fast) {
   else
     launch_contract(tabs, S, c->d_mmr, c->d_prow, nL, q0.n_T, q0.stride, c->d_eff, c->stream);
   HIP_TRY(hipGetLastError());
+  lap(4);
   SpecMeta m = c->smeta[0];
   m.tab = c->d_eff;
   if (!c->d_smeta_eff) TRY(dalloc(&c->d_smeta_eff, 1));
@@ -269,9 +287,22 @@ int build_contracted(frei_ctx* c, bool shared_fast) {
 }
 
 // Build the per-(species, layer) pressure brackets and upload all table metadata.
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int build_meta(frei_ctx* c) {
   if (!c->meta_dirty) return 0;
   if (!c->grid_set) return fail("frei_set_grid must be called before using tables");
+  double t_prev = now_ms();
+  auto lap = [&](int k) {   // frei_setup_timing phases (host wall clock, stream synced)
+    (void)hipStreamSynchronize(c->stream);
+    const double t = now_ms();
+    c->setup_ms[k] += t - t_prev;
+    t_prev = t;
+  };
+  for (double& x : c->setup_ms) x = 0.0;
   const int nL = c->nL, S = c->S;
   c->smeta.assign(S, SpecMeta{});
   c->pmeta.assign((size_t)S * nL, PMeta{});
@@ -339,6 +370,7 @@ int build_meta(frei_ctx* c) {
     }
   }
   c->fast = fast;
+  lap(0);
   // One bracket serves every species when their nodes, shapes and row pitch coincide.
   int shared = 1;
   for (int s = 1; s < S; ++s) {
@@ -367,7 +399,8 @@ int build_meta(frei_ctx* c) {
   TRY(h2d(c->d_tperm, c->tperm.data(), c->tperm.size(), c->stream));
   if (c->mmr.size() != (size_t)S * nL * c->n_atm) return fail("frei_set_mmr must be called");
   TRY(h2d(c->d_mmr, c->mmr.data(), (size_t)S * nL * c->n_atm, c->stream));
-  TRY(build_contracted(c, fast && shared));
+  lap(1);
+  TRY(build_contracted(c, fast && shared, lap));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->meta_dirty = false;
   return 0;
@@ -519,10 +552,27 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   }
   HIP_TRY(hipGetLastError());
   if (c->timing) HIP_TRY(hipEventRecord(e1, c->stream));
+  P2PPush push{};
+  P2PWait wait{};
+  if (c->d_mbox) {   // P2P: the reduce kernel pushes, the update kernel waits (no host step)
+    const uint64_t seq = ++c->p2p_seq;
+    push.peers = c->d_peers;
+    push.nranks = c->nranks;
+    push.rank = c->rank;
+    push.n = (int64_t)ns * 4;
+    push.seq = seq;
+    wait.mbox = c->d_mbox;
+    wait.nranks = c->nranks;
+    wait.n = push.n;
+    wait.seq = seq;
+    wait.timeout_ticks = (int64_t)(c->p2p_timeout_s * 1e8);   // wall_clock64: 100 MHz
+    wait.err = c->d_comm_err;
+    wait.wait_ticks = c->timing ? c->d_wait_ticks : nullptr;
+  }
   {
     const AtmStride bs = atm_stride(c);
     launch_reduce(c->d_part, nb_run, c->d_Fb, ns * 4, c->d_conv, o.force, c->stream,
-                  c->n_atm, bs.part, bs.fb);
+                  c->n_atm, bs.part, bs.fb, c->d_mbox ? &push : nullptr);
   }
   HIP_TRY(hipGetLastError());
   const double* Fb = c->d_Fb;
@@ -555,6 +605,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   if (x1) HIP_TRY(hipEventRecord(x1, c->stream));
   UpdateArgs u{};
   u.su = setup_args(c);
+  u.p2p = wait;
   u.dir = o.dir;
   u.next_dir = o.next_dir;
   u.nranks = c->nranks;
@@ -578,11 +629,11 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   u.ndiff = c->d_ndiff;
   u.iter = c->d_iter;
   u.conv = c->d_conv;
-  // metadata in LDS when the whole update stays within 64 KiB of LDS
-  const size_t S_meta = c->eff ? 1 : c->S;
-  u.meta_in_lds = (S_meta * c->nL * (sizeof(PMeta) + sizeof(double)) +
-                   S_meta * sizeof(SpecMeta) + (size_t)12 * c->nL * sizeof(double) +
-                   c->tnodes.size() * sizeof(double)) <= 64 * 1024;
+  // metadata in LDS when the update's whole allocation (the launch's own formula) fits the
+  // 64 KiB a workgroup may request
+  const int S_meta = c->eff ? 1 : c->S;
+  u.meta_in_lds = update_lds_bytes(c->nL, (int)c->tnodes.size(), S_meta, true) <=
+                  std::min<size_t>(c->lds_per_block, 64 * 1024);
   launch_update(u, c->stream, c->n_atm);
   HIP_TRY(hipGetLastError());
   return 0;
@@ -618,6 +669,7 @@ AtmStride atm_stride(frei_ctx* c) {
   b.flux = nL * c->nlam;
   b.tab = (int64_t)c->eff_stride;
   b.part = ns * 4 * (int64_t)(4 * c->nblocks);
+  b.ftoa = c->ftoa_per_atm ? c->nlam : 0;
   b.g = c->d_g;
   return b;
 }
@@ -631,12 +683,45 @@ int ensure_dtaus(frei_ctx* c) {
 
 bool ready(frei_ctx* c) { return c && c->grid_set; }
 
+// Tuning knobs (frei_set_option and FREI_<NAME> environment variables); each takes effect at
+// the next metadata build (the tables' sweep path is re-derived).
+const char* const kOptionNames[] = {"prefetch_depth", "shared", "shared_max_blocks",
+                                    "precontract", "depth4_max_blocks", "pair_max_blocks",
+                                    "quad_max_blocks", "red_rows", "red_stage", "group_q",
+                                    nullptr};
+int set_option(frei_ctx* c, const std::string& k, int v) {
+  if (k == "prefetch_depth") c->prefetch_depth = v;
+  else if (k == "shared") c->shared_mode = v < 0 ? -1 : (v ? 1 : 0);
+  else if (k == "shared_max_blocks") c->shared_max_blocks = v;
+  else if (k == "precontract") c->eff_mode = v < 0 ? -1 : (v ? 1 : 0);
+  else if (k == "depth4_max_blocks") c->depth4_max_blocks = v;
+  else if (k == "pair_max_blocks") c->pair_max_blocks = v;
+  else if (k == "quad_max_blocks") c->quad_max_blocks = v;
+  else if (k == "red_rows") c->red_rows = v != 0;
+  else if (k == "red_stage") c->red_stage = v != 0;
+  else if (k == "group_q") c->group_q = (v == 1 || v == 2 || v == 4) ? v : 0;
+  else return fail("unknown option '" + k + "'");
+  c->meta_dirty = true;
+  return 0;
+}
+
+// After a stream synchronize: did a P2P wait time out (a rank never published its sums)?
+int check_comm(frei_ctx* c) {
+  if (!c->d_comm_err) return 0;
+  int e = 0;
+  HIP_TRY(hipMemcpy(&e, c->d_comm_err, sizeof(int), hipMemcpyDeviceToHost));
+  if (e)
+    return fail("P2P exchange timed out: a peer rank did not publish its partial sums "
+                "(FREI_P2P_TIMEOUT_S)");
+  return 0;
+}
+
 }  // namespace
 
 // ==================================================================== C ABI
 extern "C" {
 
-int frei_version(void) { return 100; }
+int frei_version(void) { return 20000; }
 
 const char* frei_last_error(void) { return g_err.c_str(); }
 
@@ -663,18 +748,11 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
   c->n_atm = n_atm;
   c->sp.resize(n_species);
   c->nblocks = (int)((n_lam + kBlock - 1) / kBlock);
-  if (const char* e = getenv("FREI_PREFETCH_DEPTH")) c->prefetch_depth = atoi(e);
-  if (const char* e = getenv("FREI_SHARED")) c->shared_mode = atoi(e) ? 1 : 0;
-  if (const char* e = getenv("FREI_SHARED_MAX_BLOCKS")) c->shared_max_blocks = atoi(e);
-  if (const char* e = getenv("FREI_PRECONTRACT")) c->eff_mode = atoi(e) ? 1 : 0;
-  if (const char* e = getenv("FREI_DEPTH4_MAX_BLOCKS")) c->depth4_max_blocks = atoi(e);
-  if (const char* e = getenv("FREI_PAIR_MAX_BLOCKS")) c->pair_max_blocks = atoi(e);
-  if (const char* e = getenv("FREI_QUAD_MAX_BLOCKS")) c->quad_max_blocks = atoi(e);
-  if (const char* e = getenv("FREI_RED_ROWS")) c->red_rows = atoi(e) != 0;
-  if (const char* e = getenv("FREI_RED_STAGE")) c->red_stage = atoi(e) != 0;
-  if (const char* e = getenv("FREI_GROUP_Q")) {
-    const int q = atoi(e);
-    c->group_q = (q == 1 || q == 2 || q == 4) ? q : 0;
+  // tuning knobs: FREI_<NAME> in the environment, or frei_set_option(ctx, "<name>", v)
+  for (const char* const* k = kOptionNames; *k; ++k) {
+    std::string env = "FREI_";
+    for (const char* q = *k; *q; ++q) env += (char)std::toupper((unsigned char)*q);
+    if (const char* e = getenv(env.c_str())) (void)set_option(c, *k, atoi(e));
   }
   auto bail = [&](int rc) {
     frei_ctx_destroy(c);
@@ -682,6 +760,11 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
   };
   int rc;
   if ((rc = set_device(c))) return bail(rc);
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.sharedMemPerBlock > 0)
+      c->lds_per_block = prop.sharedMemPerBlock;
+  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail("hipStreamCreate failed"));
   const size_t NL = n_layers, NS = n_species, ns = n_layers - 1, A = n_atm;
@@ -733,6 +816,12 @@ int frei_ctx_destroy(frei_ctx* c) {
     Rccl* r = rccl();
     if (r && r->commDestroy) r->commDestroy(c->comm);
   }
+  for (void* p : c->peer_mapped) (void)hipIpcCloseMemHandle(p);
+  c->peer_mapped.clear();
+  dfree(c->d_peers);
+  dfree(c->d_mbox);
+  dfree(c->d_comm_err);
+  dfree(c->d_wait_ticks);
   for (auto& s : c->sp) dfree(s.d_tab);
   dfree(c->d_eff);
   dfree(c->d_smeta_eff);
@@ -782,6 +871,7 @@ int frei_set_grid(frei_ctx* c, const double* c1, const double* lk, const double*
   TRY(h2d(c->d_lk, lk, n, c->stream));
   TRY(h2d(c->d_sig, sigma, n, c->stream));
   TRY(h2d(c->d_ftoa, f_toa, n, c->stream));
+  c->ftoa_per_atm = false;   // one F_TOA for every atmosphere again
   TRY(h2d(c->d_wtr, trapz_w, n, c->stream));
   TRY(h2d(c->d_p, c->p.data(), c->nL, c->stream));
   launch_log_ratio(c->d_p, c->p_top2, c->nL, c->d_lnp, c->stream);
@@ -920,6 +1010,24 @@ int frei_set_mmr(frei_ctx* c, const double* mmr) {
   return 0;
 }
 
+int frei_set_ftoa_batch(frei_ctx* c, const double* f_toa) {
+  if (!c || !f_toa) return fail("null argument");
+  if (c->n_atm < 2) return fail("frei_set_ftoa_batch needs a batched context (frei_set_grid sets F_TOA)");
+  if (!c->grid_set) return fail("frei_set_grid must be called first");
+  TRY(set_device(c));
+  const size_t n = (size_t)c->nlam * c->n_atm;
+  double* d = nullptr;
+  TRY(dalloc(&d, n));
+  if (h2d(d, f_toa, n, c->stream) || hipStreamSynchronize(c->stream) != hipSuccess) {
+    dfree(d);
+    return fail("F_TOA upload failed");
+  }
+  dfree(c->d_ftoa);
+  c->d_ftoa = d;
+  c->ftoa_per_atm = true;
+  return 0;
+}
+
 int frei_set_gravity(frei_ctx* c, const double* g) {
   if (!c || !g) return fail("null argument");
   if (c->n_atm < 2) return fail("frei_set_gravity needs a batched context (frei_set_grid sets g)");
@@ -992,6 +1100,7 @@ int frei_sweep(frei_ctx* c, int direction, double alpha, double* dT, double* bol
   HIP_TRY(hipGetLastError());
   TRY(run_sweep(c, o));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  TRY(check_comm(c));
   if (dT) HIP_TRY(hipMemcpy(dT, c->d_dT, c->nL * sizeof(double), hipMemcpyDeviceToHost));
   if (bol) {
     HIP_TRY(hipMemcpy(bol, c->d_bol, c->nL * 4 * sizeof(double), hipMemcpyDeviceToHost));
@@ -1052,7 +1161,7 @@ int frei_synchronize(frei_ctx* c) {
   if (!c) return fail("null argument");
   TRY(set_device(c));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  return 0;
+  return check_comm(c);
 }
 
 int frei_run(frei_ctx* c, const double* T_init, int n_timesteps, int n_zero_crossings,
@@ -1090,6 +1199,7 @@ int frei_run(frei_ctx* c, const double* T_init, int n_timesteps, int n_zero_cros
   f.dtaus = c->d_dtaus;
   TRY(run_sweep(c, f));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  TRY(check_comm(c));
   int it = 0;
   HIP_TRY(hipMemcpy(&it, c->d_iter, sizeof(int), hipMemcpyDeviceToHost));
   *n_iter = it;
@@ -1216,23 +1326,35 @@ int frei_kappa(frei_ctx* c, double T, double p, double* k, double* sigma) {
 int frei_propagate_fluxes(int device, int64_t n, const double* c1, const double* lk,
                           const double* F_1_up, const double* F_2_down, double T_1,
                           double T_2, const double* delta_tau, const double* omega_0,
-                          double* F_2_up, double* F_1_down) {
+                          const double* g_0, double* F_2_up, double* F_1_down) {
   if (n <= 0) return 0;
   if (!c1 || !lk || !F_1_up || !F_2_down || !delta_tau || !omega_0 || !F_2_up || !F_1_down)
     return fail("null argument");
   HIP_TRY(hipSetDevice(device));
-  double* d[10] = {};
-  for (int i = 0; i < 10; ++i) TRY(dalloc(&d[i], n));
-  const double* in[6] = {c1, lk, F_1_up, F_2_down, delta_tau, omega_0};
-  for (int i = 0; i < 6; ++i)
-    HIP_TRY(hipMemcpy(d[i], in[i], n * sizeof(double), hipMemcpyHostToDevice));
-  launch_propagate(n, d[0], d[1], d[2], d[3], T_1, T_2, d[4], d[5], d[6], d[7], nullptr);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(F_2_up, d[6], n * sizeof(double), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(F_1_down, d[7], n * sizeof(double), hipMemcpyDeviceToHost));
-  for (int i = 0; i < 10; ++i) dfree(d[i]);
-  return 0;
+  // inputs c1, lk, F_1_up, F_2_down, delta_tau, omega_0 [, g_0]; outputs F_2_up, F_1_down
+  const double* in[7] = {c1, lk, F_1_up, F_2_down, delta_tau, omega_0, g_0};
+  const int n_in = g_0 ? 7 : 6;
+  double* d[9] = {};
+  hipStream_t st = nullptr;
+  int rc = 0;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
+    return fail("hipStreamCreate failed");
+  for (int i = 0; i < n_in + 2 && !rc; ++i) rc = dalloc(&d[i], n);
+  for (int i = 0; i < n_in && !rc; ++i) rc = h2d(d[i], in[i], n, st);
+  if (!rc) {
+    launch_propagate(n, d[0], d[1], d[2], d[3], T_1, T_2, d[4], d[5], g_0 ? d[6] : nullptr,
+                     d[n_in], d[n_in + 1], st);
+    if (hipGetLastError() != hipSuccess) rc = fail("propagate kernel launch failed");
+  }
+  if (!rc && (hipMemcpyAsync(F_2_up, d[n_in], n * sizeof(double), hipMemcpyDeviceToHost, st) !=
+                  hipSuccess ||
+              hipMemcpyAsync(F_1_down, d[n_in + 1], n * sizeof(double), hipMemcpyDeviceToHost,
+                             st) != hipSuccess))
+    rc = fail("propagate copy failed");
+  if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = fail("propagate kernel failed");
+  for (double*& p : d) dfree(p);
+  (void)hipStreamDestroy(st);
+  return rc;
 }
 
 int frei_comm_unique_id(void* id128) {
@@ -1290,6 +1412,75 @@ int frei_comm_init_host(frei_ctx* c, int nranks, int rank, frei_allgather_fn fn,
   c->nranks = nranks;
   c->rank = rank;
   return 0;
+}
+
+// ---- P2P exchange: mailbox + IPC handle, then map every rank's mailbox.
+int frei_comm_p2p_handle(frei_ctx* c, int nranks, int rank, void* handle64) {
+  if (c && c->n_atm > 1)
+    return fail("batched contexts shard atmospheres across ranks: no exchange");
+  if (!c || !handle64) return fail("null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail("bad rank/nranks");
+  if (c->comm || c->host_ag || c->d_mbox) return fail("communicator already initialised");
+  TRY(set_device(c));
+  const int64_t n = (int64_t)(c->nL - 1) * 4;
+  void* mb = nullptr;
+  HIP_TRY(hipExtMallocWithFlags(&mb, mbox_bytes(nranks, n), hipDeviceMallocUncached));
+  c->d_mbox = static_cast<double*>(mb);
+  HIP_TRY(hipMemset(c->d_mbox, 0, mbox_bytes(nranks, n)));   // flags 0: nothing published
+  hipIpcMemHandle_t h;
+  HIP_TRY(hipIpcGetMemHandle(&h, c->d_mbox));
+  std::memcpy(handle64, &h, sizeof(h));
+  c->nranks = nranks;
+  c->rank = rank;
+  if (const char* e = getenv("FREI_P2P_TIMEOUT_S")) c->p2p_timeout_s = atof(e);
+  return 0;
+}
+
+int frei_comm_p2p_open(frei_ctx* c, const void* handles) {
+  if (!c || !handles) return fail("null argument");
+  if (!c->d_mbox) return fail("frei_comm_p2p_handle first");
+  if (c->d_peers) return fail("P2P mailboxes already mapped");
+  TRY(set_device(c));
+  const int R = c->nranks;
+  std::vector<double*> ptr(R, nullptr);
+  for (int r = 0; r < R; ++r) {
+    if (r == c->rank) {
+      ptr[r] = c->d_mbox;
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, static_cast<const char*>(handles) + (size_t)r * sizeof(h), sizeof(h));
+    void* p = nullptr;
+    HIP_TRY(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    c->peer_mapped.push_back(p);
+    ptr[r] = static_cast<double*>(p);
+  }
+  TRY(dalloc(&c->d_peers, R));
+  TRY(h2d(c->d_peers, ptr.data(), R, c->stream));
+  TRY(dalloc(&c->d_comm_err, 1));
+  TRY(dalloc(&c->d_wait_ticks, 1));
+  HIP_TRY(hipMemsetAsync(c->d_comm_err, 0, sizeof(int), c->stream));
+  HIP_TRY(hipMemsetAsync(c->d_wait_ticks, 0, sizeof(unsigned long long), c->stream));
+  dfree(c->d_Fb_all);
+  TRY(dalloc(&c->d_Fb_all, (size_t)R * (c->nL - 1) * 4));
+  // handshake: every rank publishes flag 1 in every mailbox and waits for all (bounded)
+  P2PPush push{};
+  push.peers = c->d_peers;
+  push.nranks = R;
+  push.rank = c->rank;
+  push.n = (int64_t)(c->nL - 1) * 4;
+  push.seq = ++c->p2p_seq;
+  P2PWait wait{};
+  wait.mbox = c->d_mbox;
+  wait.nranks = R;
+  wait.n = push.n;
+  wait.seq = push.seq;
+  wait.timeout_ticks = (int64_t)(std::min(c->p2p_timeout_s, 20.0) * 1e8);
+  wait.err = c->d_comm_err;
+  launch_p2p_handshake(push, wait, c->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return check_comm(c);
 }
 
 // dtaus for post-processing: the caller's host array (uploaded) or the device copy.
@@ -1369,6 +1560,17 @@ int frei_ctx_path(frei_ctx* c, int* flags) {
   return 0;
 }
 
+int frei_set_option(frei_ctx* c, const char* name, int value) {
+  if (!c || !name) return fail("null argument");
+  return set_option(c, name, value);
+}
+
+int frei_setup_timing(frei_ctx* c, double* ms) {
+  if (!c || !ms) return fail("null argument");
+  for (int k = 0; k < 5; ++k) ms[k] = c->setup_ms[k];
+  return 0;
+}
+
 int frei_timing_enable(frei_ctx* c, int on) {
   if (!c) return fail("null argument");
   TRY(set_device(c));
@@ -1376,6 +1578,8 @@ int frei_timing_enable(frei_ctx* c, int on) {
   c->timing = on != 0;
   c->ev_used = 0;
   c->xev_used = 0;
+  if (c->d_wait_ticks)
+    HIP_TRY(hipMemset(c->d_wait_ticks, 0, sizeof(unsigned long long)));
   return 0;
 }
 
@@ -1398,6 +1602,13 @@ int frei_timing_read_exchange(frei_ctx* c, double* total_ms, int* n_calls) {
   if (!c || !total_ms || !n_calls) return fail("null argument");
   TRY(set_device(c));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->d_mbox && c->d_wait_ticks) {   // P2P: time the update kernels spent waiting
+    unsigned long long t = 0;
+    HIP_TRY(hipMemcpy(&t, c->d_wait_ticks, sizeof(t), hipMemcpyDeviceToHost));
+    *total_ms = (double)t * 1e-5;       // 100 MHz ticks
+    *n_calls = (int)(c->ev_used / 2);   // one wait per timed sweep
+    return 0;
+  }
   double tot = 0;
   for (size_t k = 0; k + 1 < c->xev_used; k += 2) {
     float ms = 0;

@@ -2,11 +2,15 @@
 
 One process per GPU; each owns the contiguous slice ``partition(n_lam, nranks, rank)``
 of the global grid.  Bolometric sums use per-point trapezoid weights of the GLOBAL grid,
-so a slice needs no halo; the only exchange is one all-gather of the per-sweep partial
-sums (n_layers x 4 doubles), summed in rank order on every rank (bitwise-identical T).
+so a slice needs no halo; the only exchange is the per-sweep partial sums (n_layers x 4
+doubles), summed in rank order on every rank (bitwise-identical T).
 
-Transports: RCCL over xGMI inside the native engine (``rccl_comm``), or a host
-all-gather through torch.distributed/gloo (``gloo_comm``) for ranks sharing a GPU.
+Transports (``Engine(comm=...)``), all set up through a plain-socket
+:class:`~frei_amd.rendezvous.Rendezvous` (no PyTorch anywhere on this path):
+- ``p2p_comm``: the engine's own device-resident exchange over xGMI — every rank pushes its
+  sums into every rank's IPC-mapped mailbox, the update kernel waits on per-value flags;
+- ``rccl_comm``: one ``ncclAllGather`` per sweep inside the engine (RCCL, dlopen'ed);
+- ``host_comm``: the per-sweep all-gather through the host (tests; ranks sharing a GPU).
 """
 import ctypes
 
@@ -14,30 +18,30 @@ import numpy as np
 
 from . import _native as N
 from .engine import partition
+from .rendezvous import Rendezvous, from_env
 
-__all__ = ["partition", "rccl_comm", "gloo_comm"]
+__all__ = ["partition", "p2p_comm", "rccl_comm", "host_comm", "Rendezvous", "from_env"]
 
 
-def rccl_comm(dist, nranks, rank):
-    """RCCL communicator spec for Engine(comm=...): rank 0 creates the unique id and
-    ``dist`` (an initialised torch.distributed) broadcasts it."""
-    uid = None
-    if rank == 0:
+def p2p_comm(rdzv):
+    """P2P mailbox spec for Engine(comm=...): the IPC handles are all-gathered through
+    ``rdzv`` once, when the engine joins."""
+    return ("p2p", rdzv.world, rdzv.rank, rdzv.all_gather)
+
+
+def rccl_comm(rdzv):
+    """RCCL communicator spec: rank 0 creates the unique id, ``rdzv`` broadcasts it."""
+    uid = b""
+    if rdzv.rank == 0:
         buf = ctypes.create_string_buffer(128)
         N.check(N.lib().frei_comm_unique_id(buf))
         uid = buf.raw
-    obj = [uid]
-    dist.broadcast_object_list(obj, src=0)
-    return ("rccl", nranks, rank, obj[0])
+    return ("rccl", rdzv.world, rdzv.rank, rdzv.broadcast(uid, src=0))
 
 
-def gloo_comm(dist, nranks, rank):
-    """Host all-gather spec (torch.distributed CPU tensors)."""
-    import torch
-
+def host_comm(rdzv):
+    """Host all-gather spec: every sweep's partial sums go through ``rdzv`` (rank order)."""
     def allgather(send):
-        t = torch.from_numpy(np.ascontiguousarray(send))
-        out = [torch.empty_like(t) for _ in range(nranks)]
-        dist.all_gather(out, t)
-        return np.concatenate([o.numpy() for o in out])
-    return ("host", nranks, rank, allgather)
+        parts = rdzv.all_gather(np.ascontiguousarray(send, dtype=np.float64).tobytes())
+        return np.concatenate([np.frombuffer(p, dtype=np.float64) for p in parts])
+    return ("host", rdzv.world, rdzv.rank, allgather)

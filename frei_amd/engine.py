@@ -112,13 +112,25 @@ class Engine:
             self._join(comm)
 
     def _join(self, comm):
-        """comm = ("rccl", nranks, rank, unique_id_bytes) or
+        """comm = ("rccl", nranks, rank, unique_id_bytes),
+        ("p2p", nranks, rank, all_gather(bytes) -> [bytes] in rank order) or
         ("host", nranks, rank, allgather(send: ndarray) -> ndarray[nranks * n])."""
         lib = N.lib()
         kind, nranks, rank, arg = comm
         if kind == "rccl":
             buf = ctypes.create_string_buffer(bytes(arg), 128)
             N.check(lib.frei_comm_init(self._ctx, nranks, rank, buf))
+        elif kind == "p2p":
+            h = ctypes.create_string_buffer(64)
+            rc = lib.frei_comm_p2p_handle(self._ctx, nranks, rank, h)
+            msg = lib.frei_last_error().decode(errors="replace") if rc else ""
+            hs = arg(h.raw if rc == 0 else b"")     # every rank joins the exchange
+            if rc != 0:
+                raise RuntimeError(f"frei_hip: {msg}")
+            if len(hs) != nranks or any(len(x) != 64 for x in hs):
+                raise RuntimeError("P2P setup failed on a peer rank (no mailbox handle)")
+            allh = ctypes.create_string_buffer(b"".join(hs), 64 * nranks)
+            N.check(lib.frei_comm_p2p_open(self._ctx, allh))
         elif kind == "host":
             def cb(send, recv, n, _user, _fn=arg, _R=nranks):
                 try:
@@ -272,6 +284,17 @@ class Engine:
         return dict(fast=bool(v & 1), lds_steps=bool(v & 2), contracted=bool(v & 4),
                     nan=bool(v & 8), paired=bool(v & 16), quad=bool(v & 32))
 
+    def set_option(self, name, value):
+        """Tuning knob of include/frei_hip.h frei_set_option (e.g. "precontract", 0)."""
+        N.check(N.lib().frei_set_option(self._ctx, name.encode(), int(value)))
+
+    def setup_timing(self):
+        """Milliseconds of the last one-time metadata build by phase (frei_setup_timing)."""
+        ms = np.zeros(5)
+        N.check(N.lib().frei_setup_timing(self._ctx, N.dptr(ms)))
+        return dict(zip(("brackets_host", "uploads", "eff_alloc", "eff_zero", "contract"),
+                        ms.tolist()))
+
     def kappa(self, T, p_bar):
         k = np.empty(self.n_lam)
         sig = np.empty(self.n_lam)
@@ -280,16 +303,68 @@ class Engine:
         return k, sig
 
 
-def propagate_fluxes_device(lam_um, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0, device=0):
-    """twostream.py:97-177 on the GPU (g_0 = 0)."""
+# ---------------------------------------------------------------------- shim engine cache
+# The reference's seam functions (emit/absorb/kappa) are stateless and a caller may drive them
+# in a Python loop, as Grid.emission_spectrum does (core.py:273-299).  A fresh context per
+# call would re-upload every opacity table (30 GB at C3), so the shims keep the last few
+# contexts, keyed on the identity of the opacity dict and its tables plus the grid arrays.
+# Tables are treated as immutable while cached: after editing table values in place, call
+# clear_engine_cache().
+_ENGINE_CACHE = []       # [(key, opacities (kept alive so its id stays unique), engine)]
+_ENGINE_CACHE_SIZE = 2
+
+
+def _array_key(a):
+    a = np.ascontiguousarray(np.asarray(a, dtype=float))
+    return (a.shape, hash(a.tobytes()))
+
+
+def _tables_key(opacities):
+    out = []
+    for name, tab in opacities.items():
+        vals = getattr(tab, "__dict__", {}).get("values")
+        ptr = vals.ctypes.data if isinstance(vals, np.ndarray) else None
+        out.append((name, id(tab), ptr))
+    return (id(opacities), tuple(out))
+
+
+def cached_engine(opacities, *, lam_um, p_bar, g, m_bar, F_toa, mmr=None, device=0):
+    """An :class:`Engine` for these tables and grid, reused across calls with the same
+    opacity dict (by identity) and equal grid arrays / scalars."""
+    key = (_tables_key(opacities), _array_key(lam_um), _array_key(p_bar), float(g),
+           float(m_bar), None if F_toa is None else _array_key(F_toa),
+           None if mmr is None else _array_key(mmr), int(device))
+    for i, (k, _, eng) in enumerate(_ENGINE_CACHE):
+        if k == key and eng._ctx:
+            _ENGINE_CACHE.insert(0, _ENGINE_CACHE.pop(i))
+            return eng
+    eng = Engine(lam_um, p_bar, opacities, g=g, m_bar=m_bar, F_toa=F_toa, mmr=mmr,
+                 device=device)
+    _ENGINE_CACHE.insert(0, (key, opacities, eng))
+    while len(_ENGINE_CACHE) > _ENGINE_CACHE_SIZE:
+        _ENGINE_CACHE.pop()[2].close()
+    return eng
+
+
+def clear_engine_cache():
+    """Release the contexts the emit/absorb/kappa shims keep between calls."""
+    while _ENGINE_CACHE:
+        _ENGINE_CACHE.pop()[2].close()
+
+
+def propagate_fluxes_device(lam_um, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0, g_0=0.0,
+                            device=0):
+    """twostream.py:97-177 on the GPU; ``g_0`` scalar or per-wavelength (0: the call sites'
+    value, twostream.py:389, 518)."""
     lam_cm = np.asarray(lam_um, dtype=float).ravel() * UM
     n = lam_cm.size
     bc = lambda a: N.f64(np.broadcast_to(np.asarray(a, dtype=float).ravel()
                                          if np.ndim(a) else a, (n,)))
     c1, lk = N.f64(planck_prefactor(lam_cm)), N.f64(lam_cm * K_B)
     F1u, F2d, dtau, w0 = bc(F_1_up), bc(F_2_down), bc(delta_tau), bc(omega_0)
+    g0 = None if np.all(np.asarray(g_0) == 0) else bc(g_0)
     F2u, F1d = np.empty(n), np.empty(n)
     N.check(N.lib().frei_propagate_fluxes(device, n, N.dptr(c1), N.dptr(lk), N.dptr(F1u),
                                           N.dptr(F2d), float(T_1), float(T_2), N.dptr(dtau),
-                                          N.dptr(w0), N.dptr(F2u), N.dptr(F1d)))
+                                          N.dptr(w0), N.dptr(g0), N.dptr(F2u), N.dptr(F1d)))
     return F2u, F1d

@@ -94,21 +94,36 @@ def sigma_scattering(lam_um, m_bar):
     return rayleigh_H2(lam_um, m_bar) + rayleigh_He(lam_um, m_bar)
 
 
+_KAPPA_P = np.array([4.0, 2.0, 1.0, 0.5])   # bar: kappa's context needs some layer grid
+
+
 def kappa(opacities, temperature, pressure, lam, m_bar=M_BAR_DEFAULT, device=0):
     """Total opacity at one (T, p): (k, sigma_scattering) in cm^2 g^-1 (opacity.py:203-269).
 
     k = sum_s mmr_s * interp_s(p, T) + sigma (linear, fill 0 outside the node hull;
     pressure-only for single-temperature tables).  Runs on the GPU."""
-    from .engine import Engine
-    lam_um = value(lam, "um")
-    T = scalar(temperature, "K")
-    p = scalar(pressure, "bar")
-    eng = Engine(lam_um, np.array([p * 4, p * 2, p, p / 2]), opacities, m_bar=m_bar,
-                 device=device)
-    try:
-        return eng.kappa(T, p)
-    finally:
-        eng.close()
+    from .engine import cached_engine
+    lam_um = np.asarray(value(lam, "um"), dtype=float)
+    T = np.asarray(value(temperature, "K"), dtype=float)
+    p = np.asarray(value(pressure, "bar"), dtype=float)
+    # one context per (tables, wavelengths, m_bar), reused across calls; its layer grid only
+    # carries the mock chemistry's (layer-independent) mixing ratios
+    eng = cached_engine(opacities, lam_um=lam_um, p_bar=_KAPPA_P, g=1.0,
+                        m_bar=scalar(m_bar, "g"), F_toa=None, device=device)
+    if T.ndim == 0 and p.ndim == 0:
+        return eng.kappa(float(T), float(p))
+    # vector mode: points along one dimension z (opacity.py:235-263).  The reference
+    # flattens the (z, lam) result before adding sigma (opacity.py:266-269), so a one-point
+    # array gives a flat k; for z > 1 its broadcast fails, and here k is (z, lam).
+    Tz, pz = np.broadcast_arrays(T, p)
+    ks = []
+    sig = None
+    for Tq, pq in zip(Tz.ravel(), pz.ravel()):
+        k, sig = eng.kappa(float(Tq), float(pq))
+        ks.append(k)
+    if len(ks) == 1:
+        return ks[0], sig
+    return np.array(ks).reshape(Tz.shape + (lam_um.size,)), sig
 
 
 def load_example_opacity(grid, seed=42, scale_factor=20):

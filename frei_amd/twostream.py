@@ -8,7 +8,7 @@ m_bar g (astropy Quantities are accepted and converted when astropy is installed
 import numpy as np
 
 from .constants import C, H, K_B, M_BAR_DEFAULT, UM
-from .engine import ABSORB, EMIT, Engine, propagate_fluxes_device
+from .engine import ABSORB, EMIT, cached_engine, propagate_fluxes_device
 from .units import scalar, value
 
 __all__ = ["propagate_fluxes", "emit", "absorb", "BB", "E"]
@@ -34,48 +34,47 @@ def E(omega_0, g_0):
 def propagate_fluxes(lam, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0=0, g_0=0, eps=0.5,
                      device=0):
     """Improved two-stream update of one layer pair, elementwise over wavelength
-    (twostream.py:97-177) -> (F_2_up, F_1_down).  The engine implements the g_0 = 0
-    case every call site uses (twostream.py:389, 518); ``eps`` is unused as in the
-    reference."""
-    if np.any(np.asarray(g_0) != 0):
-        raise ValueError("propagate_fluxes: only g_0 = 0 is implemented (as used by emit/absorb)")
+    (twostream.py:97-177) -> (F_2_up, F_1_down).  ``g_0`` (scalar or per wavelength) enters
+    E, the transmission, zeta and B' through (1 - omega_0 g_0) as in the reference; emit and
+    absorb use g_0 = 0 (twostream.py:389, 518).  ``eps`` is unused as in the reference."""
     flux = "erg / (s cm3)"
     return propagate_fluxes_device(value(lam, "um"), value(F_1_up, flux), value(F_2_down, flux),
                                    scalar(T_1, "K"), scalar(T_2, "K"),
                                    np.asarray(delta_tau, dtype=float),
-                                   np.asarray(omega_0, dtype=float), device=device)
+                                   np.asarray(omega_0, dtype=float),
+                                   g_0=np.asarray(g_0, dtype=float), device=device)
 
 
 def _sweeps(direction, opacities, temperatures, pressures, lam, F_TOA, g, m_bar, n_timesteps,
             convergence_thresh, alpha, fluxes_up, fluxes_down, device):
     T = np.array(value(temperatures, "K"), dtype=float)
-    p = value(pressures, "bar")
-    lam_um = value(lam, "um")
+    p = np.asarray(value(pressures, "bar"), dtype=float)
+    lam_um = np.asarray(value(lam, "um"), dtype=float)
     nL, nlam = p.size, lam_um.size
     ftoa = np.asarray(value(F_TOA, "erg / (s cm3)"), dtype=float)
-    eng = Engine(lam_um, p, opacities, g=g, m_bar=m_bar, F_toa=ftoa, device=device)
-    try:
-        up_in, down_in = fluxes_up, fluxes_down
-        up = np.zeros((nL, nlam)) if up_in is None else np.array(value(up_in, "erg / (s cm3)"))
-        down = (np.zeros((nL, nlam)) if down_in is None
-                else np.array(value(down_in, "erg / (s cm3)")))
-        if up_in is None and direction == ABSORB:
-            up[0] = np.pi * BB(T[0])(lam_um)          # twostream.py:468-470 (Q5)
-        if down_in is None:
-            down[-1] = ftoa                            # twostream.py:337-339, 472-474
-        eng.set_fluxes(up, down)
-        hist = np.zeros((nL, n_timesteps + 1))
-        hist[:, 0] = T
-        dtaus = dT = None
-        for j in range(n_timesteps):
-            eng.set_temperatures(hist[:, j])
-            dT, _, dtaus = eng.sweep(direction, alpha=alpha)
-            hist[:, j + 1] = hist[:, j] - dT
-            if n_timesteps > 1 and np.abs(dT).max() < convergence_thresh:
-                break
-        up, down = eng.get_fluxes()
-    finally:
-        eng.close()
+    thresh = scalar(convergence_thresh, "K")
+    # the context (uploaded tables) is reused by later calls with the same opacity dict
+    eng = cached_engine(opacities, lam_um=lam_um, p_bar=p, g=scalar(g, "cm / s2"),
+                        m_bar=scalar(m_bar, "g"), F_toa=ftoa, device=device)
+    up_in, down_in = fluxes_up, fluxes_down
+    up = np.zeros((nL, nlam)) if up_in is None else np.array(value(up_in, "erg / (s cm3)"))
+    down = (np.zeros((nL, nlam)) if down_in is None
+            else np.array(value(down_in, "erg / (s cm3)")))
+    if up_in is None and direction == ABSORB:
+        up[0] = np.pi * BB(T[0])(lam_um)          # twostream.py:468-470 (Q5)
+    if down_in is None:
+        down[-1] = ftoa                            # twostream.py:337-339, 472-474
+    eng.set_fluxes(up, down)
+    hist = np.zeros((nL, n_timesteps + 1))
+    hist[:, 0] = T
+    dtaus = dT = None
+    for j in range(n_timesteps):
+        eng.set_temperatures(hist[:, j])
+        dT, _, dtaus = eng.sweep(direction, alpha=alpha)
+        hist[:, j + 1] = hist[:, j] - dT
+        if n_timesteps > 1 and np.abs(dT).max() < thresh:
+            break
+    up, down = eng.get_fluxes()
     # the reference mutates the caller's arrays in place
     if isinstance(up_in, np.ndarray) and up_in.dtype == np.float64:
         up_in[...] = up

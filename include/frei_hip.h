@@ -41,7 +41,7 @@ typedef struct frei_ctx frei_ctx;
 
 enum { FREI_EMIT = 0, FREI_ABSORB = 1 };
 
-/* Library/ABI version (major*10000 + minor*100 + patch). */
+/* Library/ABI version (major*10000 + minor*100 + patch); 2.0.0. */
 int frei_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char* frei_last_error(void);
@@ -64,6 +64,9 @@ int frei_ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, int
 int frei_ctx_create_batch(frei_ctx** out, int device, int n_layers, int64_t n_lam,
                           int n_species, int n_atm);
 int frei_set_gravity(frei_ctx* ctx, const double* g);
+/* Batched: one F_TOA per atmosphere, f_toa[n_atm][n_lam] (core.py:48-55 with each planet's
+ * T_star and a/R_star; replaces frei_set_grid's shared F_TOA until the next frei_set_grid). */
+int frei_set_ftoa_batch(frei_ctx* ctx, const double* f_toa);
 /* Every atmosphere iterates to its own convergence (core.py:273-318), then the final emit;
  * n_iter[n_atm], T_final[n_atm][n_layers] and spectra[n_atm][n_lam] (F_up[n_layers-1]). */
 int frei_run_batch(frei_ctx* ctx, const double* T_init, int n_timesteps, int n_zero_crossings,
@@ -148,16 +151,30 @@ int frei_synchronize(frei_ctx* ctx);
  * sigma[n_lam] (may be NULL). */
 int frei_kappa(frei_ctx* ctx, double T, double p, double* k, double* sigma);
 
-/* propagate_fluxes (twostream.py:97-177), elementwise on n points, g_0 = 0. */
+/* propagate_fluxes (twostream.py:97-177), elementwise on n points; g_0[n] is the scattering
+ * asymmetry factor (NULL: g_0 = 0, as at the emit/absorb call sites twostream.py:389, 518). */
 int frei_propagate_fluxes(int device, int64_t n, const double* c1, const double* lk,
                           const double* F_1_up, const double* F_2_down, double T_1,
                           double T_2, const double* delta_tau, const double* omega_0,
-                          double* F_2_up, double* F_1_down);
+                          const double* g_0, double* F_2_up, double* F_1_down);
 
 /* Multi-GPU: 128-byte RCCL unique id (rank 0 creates, others receive it out of band),
  * then every rank joins.  Per sweep: one ncclAllGather of n_layers*4 doubles. */
 int frei_comm_unique_id(void* id128);
 int frei_comm_init(frei_ctx* ctx, int nranks, int rank, const void* id128);
+
+/*
+ * P2P exchange over xGMI without RCCL or the host: each rank allocates a
+ * mailbox in uncached device memory and exports its 64-byte IPC handle
+ * (frei_comm_p2p_handle); after the handles are all-gathered out of band (rank order),
+ * frei_comm_p2p_open maps every rank's mailbox and runs a bounded handshake.  Per sweep the
+ * reduce kernel pushes this rank's n_layers*4 partial sums into every mailbox with a
+ * sequence flag per value, and the update kernel waits for every rank's flags (a rank that
+ * never publishes is reported as an error after FREI_P2P_TIMEOUT_S seconds, default 30).
+ * Ranks may share one GPU (processes on the same device).
+ */
+int frei_comm_p2p_handle(frei_ctx* ctx, int nranks, int rank, void* handle64);
+int frei_comm_p2p_open(frei_ctx* ctx, const void* handles);
 
 /* Alternative exchange for testing and for hosts without RCCL peers (e.g. several ranks
  * sharing one GPU): per sweep the n partial sums are copied to the host and
@@ -189,12 +206,25 @@ int frei_contribution(frei_ctx* ctx, const double* dtaus, const double* nu,
  * lanes per wavelength (small slices). */
 int frei_ctx_path(frei_ctx* ctx, int* flags);
 
+/* Tuning knobs (also FREI_<NAME> in the environment at context creation): "precontract"
+ * (K3 species contraction: 1 on when it applies / 0 off / -1 automatic), "group_q" (lanes per
+ * wavelength 1, 2, 4 or 0 = automatic), "shared" (LDS step table 1/0/-1), "prefetch_depth",
+ * "shared_max_blocks", "pair_max_blocks", "quad_max_blocks", "depth4_max_blocks",
+ * "red_rows", "red_stage".  Takes effect at the next metadata build. */
+int frei_set_option(frei_ctx* ctx, const char* name, int value);
+/* Host wall-clock milliseconds of the last metadata build (the one-time setup before the
+ * first sweep after tables/mmr change), by phase: [0] per-(species, layer) brackets on the
+ * host, [1] metadata uploads, [2] contracted-table allocation, [3] its zero fill, [4] the K3
+ * contraction kernel. */
+int frei_setup_timing(frei_ctx* ctx, double* ms5);
+
 /* Timing of the sweep kernel (HIP events on the context stream around every sweep
  * launch while enabled): total milliseconds and number of timed launches. */
 int frei_timing_enable(frei_ctx* ctx, int on);
 int frei_timing_read(frei_ctx* ctx, double* total_ms, int* n_launches);
 /* While timing is enabled, also HIP events around each sweep's rank exchange (the RCCL
- * all-gather of the bolometric partials, or the host hook): total ms and number of calls. */
+ * all-gather of the bolometric partials, or the host hook): total ms and number of calls.
+ * With the P2P exchange: the time the update kernels spent waiting for peers' sums. */
 int frei_timing_read_exchange(frei_ctx* ctx, double* total_ms, int* n_calls);
 
 /*

@@ -101,7 +101,7 @@ def propagate_fluxes(lam_cm, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0=0.0,
 
 
 def propagate_error_bound(lam_cm, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0,
-                          err_F1u=0.0, err_F2d=0.0, delta=np.finfo(float).eps):
+                          err_F1u=0.0, err_F2d=0.0, delta=np.finfo(float).eps, g_0=0.0):
     """First-order forward rounding-error bound of propagate_fluxes (test infrastructure).
 
     The reference formula is ill-conditioned for thin layers: ``1 - T**2`` and
@@ -114,10 +114,11 @@ def propagate_error_bound(lam_cm, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0
     """
     w = np.asarray(omega_0, dtype=float)
     dtau = np.asarray(delta_tau, dtype=float)
-    Ev = E(w, 0.0)
-    arg = 2 * (Ev * (Ev - w)) ** 0.5 * dtau
+    Ev = E(w, g_0)
+    wg = 1 - w * g_0
+    arg = 2 * (Ev * (Ev - w) * wg) ** 0.5 * dtau
     Tr = np.exp(-arg)
-    r = ((Ev - w) / Ev) ** 0.5
+    r = ((Ev - w) / Ev / wg) ** 0.5
     zp, zm = 0.5 * (1 + r), 0.5 * (1 - r)
     chi = zm ** 2 * Tr ** 2 - zp ** 2
     xi = zp * zm * (1 - Tr ** 2)
@@ -127,7 +128,7 @@ def propagate_error_bound(lam_cm, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0
     x1 = H * C / (lam_cm * K_B * T_1)
     x2 = H * C / (lam_cm * K_B * T_2)
     m1, m2 = np.abs(B1) * (1 + x1), np.abs(B2) * (1 + x2)
-    den = 2 * Ev
+    den = 2 * Ev * wg
     mxi = np.abs(xi) + np.abs(zp * zm) * 2 * (1 + arg)
     cb = (np.abs((B1 - B2) / dtau / den) * (np.abs(chi) + np.abs(psi) + np.abs(xi))
           + (m1 + m2) / (dtau * den) * np.abs(chi - psi - xi))
@@ -136,6 +137,13 @@ def propagate_error_bound(lam_cm, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0
                + np.abs(pi) * (m2 * np.abs(chi + xi) + np.abs(psi) * m1 + cb))
     cd = ic * (np.abs(psi * F_2_down) + mxi * np.abs(F_1_up)
                + np.abs(pi) * (m1 * np.abs(chi + xi) + np.abs(psi) * m2 + cb))
+    if np.any(np.asarray(g_0) != 0):
+        # with g_0 != 0, E - omega_0 can cancel (it reaches 0 where the reference gives NaN):
+        # a relative operand error delta becomes delta (|E| + |omega_0|) / |E - omega_0| in
+        # E - omega_0, which feeds the transmission, zeta and pi
+        with np.errstate(divide="ignore", invalid="ignore"):
+            kE = (np.abs(Ev) + np.abs(w)) / np.abs(Ev - w)
+        cu, cd = cu * np.maximum(kE, 1.0), cd * np.maximum(kE, 1.0)
     e_up = delta * cu + ic * (np.abs(psi) * err_F1u + np.abs(xi) * err_F2d)
     e_dn = delta * cd + ic * (np.abs(psi) * err_F2d + np.abs(xi) * err_F1u)
     return e_up, e_dn

@@ -158,6 +158,31 @@ def case_propagate():
     save("propagate.npz", **out)
 
 
+def case_propagate_g0():
+    """propagate_fluxes with a nonzero asymmetry factor g_0 (twostream.py:139-176): array
+    g_0 of both signs, a scalar g_0, omega_0 on both sides of E's 0.1 branch."""
+    rng = np.random.default_rng(4321)
+    n = 1024
+    lam = np.logspace(np.log10(0.5), np.log10(10), n) * u.um
+    cases = [(2000.0, 1900.0, "array"), (800.0, 780.0, "array"), (1500.0, 1500.0, 0.35),
+             (3000.0, 3300.0, -0.2)]
+    out = dict(lam=lam.value)
+    for c, (T1, T2, g0) in enumerate(cases):
+        dtau = 10 ** rng.uniform(-7, 3, n)
+        omega = rng.uniform(0.0, 0.95, n)
+        g = rng.uniform(-0.9, 0.9, n) if isinstance(g0, str) else np.float64(g0)
+        F1u = 10 ** rng.uniform(8, 13, n) * FLUX
+        F2d = 10 ** rng.uniform(6, 12, n) * FLUX
+        F2u, F1d = R.twostream.propagate_fluxes(lam, F1u, F2d, T1 * u.K, T2 * u.K,
+                                                dtau, omega_0=omega, g_0=g)
+        out.update({f"c{c}_T1": T1, f"c{c}_T2": T2, f"c{c}_dtau": dtau,
+                    f"c{c}_omega": omega, f"c{c}_g0": g, f"c{c}_F1u": F1u.value,
+                    f"c{c}_F2d": F2d.value, f"c{c}_F2u": F2u.to(FLUX).value,
+                    f"c{c}_F1d": F1d.to(FLUX).value})
+    out["n_cases"] = len(cases)
+    save("propagate_g0.npz", **out)
+
+
 def separable_table(rng, lam_um, p_bar, T_nodes, lo=1e-4, hi=1e3, n_lines=200):
     """Synthetic log-normal line forest (SURVEY.md §8(d) C2 recipe), separable in (p, T)."""
     n = lam_um.size

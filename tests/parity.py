@@ -13,6 +13,11 @@ for one sweep from identical inputs, the observed relative T difference after
 T-P iterations).  Where the formula is well conditioned this is the plain 1e-10
 relative bound; the row-normwise error (max|dx| / max|ref| per layer row) is
 reported beside it.
+
+Grid-level runs are additionally held to SURVEY.md §8(c)'s stated claim
+(``assert_grid_parity``): row-normwise <= 1e-10 on the F_up / F_down layer rows and
+elementwise <= 1e-10 on the emergent spectrum F_up[-1].  The cond bound above stays as the
+per-element diagnostic for the interior fluxes.
 """
 import numpy as np
 
@@ -49,3 +54,16 @@ def assert_flux_parity(x, ref, cond, delta=EPS, what=""):
     r = bound_ratio(x, ref, cond, delta)
     assert r <= 1.0, (f"{what}: |dx| exceeds 1e-10|ref| + {K_BOUND}*delta*cond by {r:.3g}x "
                       f"(row-normwise {row_normwise(x, ref):.3g})")
+
+
+def assert_grid_parity(spectrum, ref_spectrum, up=None, ref_up=None, down=None, ref_down=None,
+                       what=""):
+    """emergent spectrum elementwise <= 1e-10 relative; F_up / F_down rows
+    normwise (max|dx| / max|ref| per layer row) <= 1e-10."""
+    r = rel(spectrum, ref_spectrum)
+    assert r <= RTOL, f"{what}: emergent spectrum elementwise {r:.3g} > 1e-10"
+    for x, ref, name in ((up, ref_up, "F_up"), (down, ref_down, "F_down")):
+        if x is None:
+            continue
+        rn = row_normwise(x, ref)
+        assert rn <= RTOL, f"{what}: {name} row-normwise {rn:.3g} > 1e-10"

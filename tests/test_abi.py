@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     lib = N.lib()
     for name in _declared():
         assert hasattr(lib, name), name
-    assert lib.frei_version() == 100
+    assert lib.frei_version() == 20000
     assert lib.frei_last_error() == b""
 
 

@@ -1,7 +1,8 @@
-"""Wavelength sharding design on CPU (gloo, world_size 2): each rank sweeps its slice
-(frei_amd.engine.partition) and all-gathers per-layer partial bolometric sums built
-with the global per-point trapezoid weights (frei_amd.engine.trapz_weights); summing
-them in rank order must reproduce the unsharded reference path."""
+"""Wavelength sharding design on CPU (world_size 2, over gloo and over the engine's
+torch-free socket transport): each rank sweeps its slice (frei_amd.engine.partition) and
+all-gathers per-layer partial bolometric sums built with the global per-point trapezoid
+weights (frei_amd.engine.trapz_weights); summing them in rank order must reproduce the
+unsharded reference path."""
 import os
 import socket
 
@@ -36,38 +37,55 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
-    import torch
-    import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, port, q, transport):
     lam, p, T0, tabs = _problem()
     lo, hi = partition(lam.size, world, rank)
     w = trapz_weights(lam * 1e-4)[lo:hi]
+    if transport == "gloo":
+        import torch
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+        def allgather(part):
+            t = torch.tensor(part, dtype=torch.float64)
+            out = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(out, t)
+            return [o.numpy() for o in out]
+    else:   # the engine's torch-free host transport (frei_amd.distributed.host_comm)
+        from frei_amd.distributed import host_comm
+        from frei_amd.rendezvous import Rendezvous
+        rdzv = Rendezvous(world, rank, addr=("127.0.0.1", port))
+        fn = host_comm(rdzv)[3]
+
+        def allgather(part):
+            return list(fn(np.asarray(part)).reshape(world, 4))
 
     def bol(F2u, F2d, F1u, F1d):
-        part = torch.tensor([np.sum(w * F2u), np.sum(w * F2d), np.sum(w * F1u),
-                             np.sum(w * F1d)], dtype=torch.float64)
-        out = [torch.empty_like(part) for _ in range(world)]
-        dist.all_gather(out, part)
-        tot = out[0].clone()
+        part = [np.sum(w * F2u), np.sum(w * F2d), np.sum(w * F1u), np.sum(w * F1d)]
+        out = allgather(part)
+        tot = np.array(out[0], dtype=float)
         for r in range(1, world):     # rank order: identical on every rank
-            tot += out[r]
+            tot = tot + out[r]
         return tuple(float(x) for x in tot)
 
     sp, T, th, dtaus, fu, fd, it = O.emission_spectrum(
         _slice_tabs(tabs, lo, hi), T0, p, lam[lo:hi], O.F_TOA(lam[lo:hi]), G_J, M_BAR, 1,
         n_timesteps=3, bol_fn=bol)
     q.put((rank, lo, hi, sp, T, th))
-    dist.destroy_process_group()
+    if transport == "gloo":
+        dist.destroy_process_group()
+    else:
+        rdzv.close()
 
 
-def test_two_rank_lambda_sharding_matches_unsharded():
-    import torch.multiprocessing as mp
+@pytest.mark.parametrize("transport", ["gloo", "sockets"])
+def test_two_rank_lambda_sharding_matches_unsharded(transport):
+    import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, transport)) for r in range(2)]
     for pr in procs:
         pr.start()
     res = sorted([q.get(timeout=240) for _ in procs], key=lambda x: x[0])

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from oracle import frei_oracle as O
-from tests.parity import EPS, assert_flux_parity, rel, row_normwise
+from tests.parity import EPS, assert_flux_parity, assert_grid_parity, rel, row_normwise
 
 pytestmark = pytest.mark.gpu
 
@@ -51,6 +51,7 @@ def test_batched_atmospheres_match_oracle_per_atmosphere(fa):
     try:
         assert eng.path()["contracted"]
         out = eng.run(T0, n_timesteps=40, n_zero_crossings=2, convergence_dT=3.0, alpha=1.0)
+        ups, downs = eng.get_fluxes()
     finally:
         eng.close()
     for m in range(5):
@@ -63,6 +64,7 @@ def test_batched_atmospheres_match_oracle_per_atmosphere(fa):
         assert relT < 1e-10, f"atmosphere {m}: T {relT:.3e}"
         assert_flux_parity(out["spectra"][m], osp, cond["up"][-1], max(EPS, relT),
                            f"atmosphere {m} spectrum")
+        assert_grid_parity(out["spectra"][m], osp, ups[m], ou, downs[m], od, f"atmosphere {m}")
 
 
 def test_batched_mfma_contraction_tiles_and_padding(fa):
@@ -102,9 +104,15 @@ def test_batched_emission_spectra_over_grids(fa):
     lam, _, _ = O.wavelength_grid(0.5, 10, 1024)
     grids = []
     op = None
-    for T_ref, g in [(1400, 1500.0), (2000, 2478.6519476149147), (2400, 4000.0)]:
+    # planets that also differ in their star (T_star) and orbit (a/R_star): each atmosphere
+    # gets its own F_TOA
+    for T_ref, g, T_star, a_r in [(1400, 1500.0, 5800.0, 6.450964670116429),
+                                  (2000, 2478.6519476149147, 4500.0, 5.0),
+                                  (2400, 4000.0, 6500.0, 8.0)]:
         pl = fa.Planet.from_hot_jupiter()
         pl.g = g
+        pl.T_star = T_star
+        pl.a_rstar = a_r
         gr = fa.Grid(pl, lam=lam, n_layers=20, T_ref=T_ref)
         if op is None:
             op = fa.load_example_opacity(gr, scale_factor=2)
@@ -116,4 +124,4 @@ def test_batched_emission_spectra_over_grids(fa):
         gr._close_engine()
         assert it == th1.shape[1] // 2
         assert rel(T, T1) < 1e-10
-        assert row_normwise(spec.flux, s1.flux) < 1e-9
+        assert rel(spec.flux, s1.flux) < 1e-10

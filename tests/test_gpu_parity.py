@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from oracle import frei_oracle as O
-from tests.parity import EPS, assert_flux_parity, rel, row_normwise
+from tests.parity import EPS, assert_flux_parity, assert_grid_parity, rel, row_normwise
 
 pytestmark = pytest.mark.gpu
 
@@ -39,9 +39,35 @@ def test_propagate_fluxes_matches_reference(fa, golden):
         assert_flux_parity(F1d, o1d, cd, what=f"case{c} F_1_down vs oracle")
 
 
-def test_propagate_fluxes_rejects_nonzero_g0(fa):
-    with pytest.raises(ValueError):
-        fa.propagate_fluxes([1.0, 2.0], [1, 1], [1, 1], 1000, 900, [1, 1], [0, 0], g_0=0.5)
+def test_propagate_fluxes_nonzero_g0_matches_reference(fa, golden):
+    """g_0 != 0 (per-wavelength arrays of both signs and scalars) against the reference's
+    own outputs; lanes where E < omega_0 are NaN in the reference and must be NaN here."""
+    P = golden("propagate_g0.npz")
+    for c in range(int(P["n_cases"])):
+        g0 = P[f"c{c}_g0"]
+        args = (P["lam"] * 1e-4, P[f"c{c}_F1u"], P[f"c{c}_F2d"], float(P[f"c{c}_T1"]),
+                float(P[f"c{c}_T2"]), P[f"c{c}_dtau"], P[f"c{c}_omega"])
+        F2u, F1d = fa.propagate_fluxes(P["lam"], P[f"c{c}_F1u"], P[f"c{c}_F2d"], args[3],
+                                       args[4], P[f"c{c}_dtau"], P[f"c{c}_omega"], g_0=g0)
+        with np.errstate(invalid="ignore"):
+            cu, cd = O.propagate_error_bound(*args, delta=1.0, g_0=g0)
+            o2u, o1d = O.propagate_fluxes(*args, g_0=g0)
+        bad = np.isnan(P[f"c{c}_F2u"])
+        assert np.array_equal(np.isnan(F2u), bad) and np.array_equal(np.isnan(F1d), bad)
+        ok = ~bad
+        for x, ref, cb, what in ((F2u, P[f"c{c}_F2u"], cu, "F_2_up"),
+                                 (F1d, P[f"c{c}_F1d"], cd, "F_1_down"),
+                                 (F2u, o2u, cu, "F_2_up vs oracle"),
+                                 (F1d, o1d, cd, "F_1_down vs oracle")):
+            assert_flux_parity(x[ok], ref[ok], cb[ok], what=f"g0 case{c} {what}")
+    # g_0 = 0 passed explicitly is the emit/absorb form
+    P0 = golden("propagate.npz")
+    a = fa.propagate_fluxes(P0["lam"], P0["c0_F1u"], P0["c0_F2d"], float(P0["c0_T1"]),
+                            float(P0["c0_T2"]), P0["c0_dtau"], P0["c0_omega"], g_0=0.0)
+    b = fa.propagate_fluxes(P0["lam"], P0["c0_F1u"], P0["c0_F2d"], float(P0["c0_T1"]),
+                            float(P0["c0_T2"]), P0["c0_dtau"], P0["c0_omega"],
+                            g_0=np.zeros(P0["lam"].size))
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
 def test_kappa_matches_reference(fa, golden):
@@ -243,6 +269,8 @@ def _grid_run(fa, C, pre, tabs_f, tabs_o, lam, p, T0, n, Ft=None):
     up, down = grid.engine().get_fluxes()
     assert_flux_parity(up, C[pre + "F_up"], cond["up"], delta, pre + "F_up")
     assert_flux_parity(down, C[pre + "F_down"], cond["down"], delta, pre + "F_down")
+    assert_grid_parity(spec.flux, C[pre + "spectrum"], up, C[pre + "F_up"], down,
+                       C[pre + "F_down"], pre + " vs reference")
     return grid, spec, T, dtaus
 
 
@@ -317,6 +345,7 @@ def test_eight_species_device_tables_match_oracle(fa):
     up, down = grid.engine().get_fluxes()
     assert_flux_parity(up, ou, cond["up"], delta, "F_up")
     assert_flux_parity(down, od, cond["down"], delta, "F_down")
+    assert_grid_parity(spec.flux, osp, up, ou, down, od, "8 species")
     assert row_normwise(dtaus, odt) < 1e-10
 
 
@@ -342,11 +371,13 @@ def test_nan_in_table_is_skipped_like_xarray_sum(fa):
     grid.load_opacities(opacities=tabs_f)
     spec, T, th, dtaus = grid.emission_spectrum(n_timesteps=2)
     cond = _cond((16, lam.size))
-    osp, oT, *_ = O.emission_spectrum(tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1,
-                                      n_timesteps=2, err=cond)
+    osp, oT, oth, odt, ou, od, it = O.emission_spectrum(tabs_o, T0, p, lam, O.F_TOA(lam), G_J,
+                                                        M_BAR, 1, n_timesteps=2, err=cond)
     relT = rel(T, oT)
     assert relT < 1e-10 and np.all(np.isfinite(spec.flux))
     assert_flux_parity(spec.flux, osp, cond["up"][-1], max(EPS, relT), "spectrum with NaN band")
+    up, down = grid.engine().get_fluxes()
+    assert_grid_parity(spec.flux, osp, up, ou, down, od, "NaN band")
 
 
 @pytest.mark.parametrize("mode", ["single_T", "offnode_p", "mixed_T"])
@@ -386,6 +417,7 @@ def test_generic_sweep_path_matches_oracle(fa, mode):
     up, down = grid.engine().get_fluxes()
     assert_flux_parity(up, ou, cond["up"], delta, mode + " F_up")
     assert_flux_parity(down, od, cond["down"], delta, mode + " F_down")
+    assert_grid_parity(spec.flux, osp, up, ou, down, od, mode)
     assert row_normwise(dtaus, odt) < 1e-10
 
 
@@ -430,6 +462,8 @@ def test_species_contraction_matches_per_species_sum(fa, monkeypatch):
         up, down = out[mode]["fluxes"]
         assert_flux_parity(up, ou, cond["up"], delta, "F_up " + mode)
         assert_flux_parity(down, od, cond["down"], delta, "F_down " + mode)
+        assert_grid_parity(out[mode]["spectrum"], osp, up, ou, down, od,
+                           "contracted" if mode == "1" else "per-species")
 
 
 @pytest.mark.parametrize("red_mode", ["stage", "rows", "full"])   # partial-sum layouts
@@ -478,3 +512,38 @@ def test_grouped_lane_sweep_matches_one_lane_form(fa, monkeypatch, n_layers, red
             assert np.all(np.abs(dT_p - dT_o) <= 1e-10 * np.abs(dT_o) + 1e-300)
         assert rel(out[q]["run"]["final_T"], out[1]["run"]["final_T"]) < 1e-12
         assert row_normwise(out[q]["run"]["spectrum"], out[1]["run"]["spectrum"]) < 1e-9
+
+
+def test_shims_reuse_device_context_and_vector_kappa(fa, golden):
+    """emit/absorb/kappa keep their device context (uploaded tables) between calls with the
+    same opacity dict: repeated calls hit the cache and give bitwise-identical results; kappa
+    also takes arrays of (T, p) points along one dimension (opacity.py:235-263)."""
+    from frei_amd import engine as E
+    E.clear_engine_cache()
+    s = golden("setup_c1.npz")
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), T_ref=2400)
+    op = fa.load_example_opacity(grid, scale_factor=1)
+    args = (op, grid.init_temperatures, grid.pressures, grid.lam, s["F_TOA"], G_J)
+    r1 = fa.emit(*args, m_bar=M_BAR, n_timesteps=1)
+    assert len(E._ENGINE_CACHE) == 1
+    eng = E._ENGINE_CACHE[0][2]
+    r2 = fa.emit(*args, m_bar=M_BAR, n_timesteps=1)
+    r3 = fa.absorb(*args, m_bar=M_BAR, n_timesteps=1)
+    assert len(E._ENGINE_CACHE) == 1 and E._ENGINE_CACHE[0][2] is eng
+    for x, y in zip(r1, r2):
+        assert np.array_equal(x, y)
+    EA = golden("emit_absorb_c1.npz")
+    assert rel(r3[2], EA["absorb_T"]) < 1e-12
+    K = golden("kappa.npz")
+    ks = [fa.kappa(op, K["ex_T"][j], K["ex_p"][j], s["lam"], m_bar=M_BAR)[0]
+          for j in range(len(K["ex_T"]))]
+    assert len(E._ENGINE_CACHE) == 2                  # one kappa context for all points
+    kv, sig = fa.kappa(op, K["ex_T"], K["ex_p"], s["lam"], m_bar=M_BAR)
+    assert kv.shape == (len(K["ex_T"]), s["lam"].size)
+    for j in range(len(K["ex_T"])):
+        assert np.array_equal(kv[j], ks[j])
+        assert rel(kv[j], K["ex_k"][j]) < 1e-13
+    k1, _ = fa.kappa(op, K["ex_T"][:1], K["ex_p"][:1], s["lam"], m_bar=M_BAR)
+    assert k1.shape == (s["lam"].size,)               # one point: flat, like the reference
+    E.clear_engine_cache()
+    assert not E._ENGINE_CACHE and eng._ctx is None
