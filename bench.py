@@ -285,7 +285,15 @@ def main():
     from frei_amd.workloads import bytes_per_update, c3
 
     if a.comm == "host":   # rehearsal: ranks may share the GPUs there are
-        d.local = d.local % max(1, N.device_count())
+        n_dev = max(1, N.device_count())
+        if d.world > n_dev and d.local >= n_dev:
+            # ranks sharing a device need distinct device address layouts
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            hip.hipSetDevice(d.local % n_dev)
+            _pad = ctypes.c_void_p()
+            hip.hipMalloc(ctypes.byref(_pad), ctypes.c_size_t((d.local // n_dev) * 1536 << 20))
+        d.local = d.local % n_dev
     w = c3(n_layers=a.n_layers, n_lam=a.n_lam, n_T=a.n_T)
     nL, n_lam, S = a.n_layers, a.n_lam, len(w["names"])
     lo, hi = partition(n_lam, d.world, d.rank)

@@ -8,7 +8,8 @@ import numpy as np
 import pytest
 
 from oracle import frei_oracle as O
-from tests.parity import EPS, assert_flux_parity, assert_grid_parity, rel, row_normwise
+from tests.parity import (EPS, assert_flux_parity, assert_grid_parity, grid_floor,
+                          perturbed_exp, rel, row_normwise)
 
 pytestmark = pytest.mark.gpu
 
@@ -64,7 +65,13 @@ def test_batched_atmospheres_match_oracle_per_atmosphere(fa):
         assert relT < 1e-10, f"atmosphere {m}: T {relT:.3e}"
         assert_flux_parity(out["spectra"][m], osp, cond["up"][-1], max(EPS, relT),
                            f"atmosphere {m} spectrum")
-        assert_grid_parity(out["spectra"][m], osp, ups[m], ou, downs[m], od, f"atmosphere {m}")
+        with perturbed_exp():
+            psp, _, _, _, pu, pd, _ = O.emission_spectrum(
+                tabs_o, T0[m], p, lam, Ft, g[m], M_BAR, 1, n_timesteps=40, n_zero_crossings=2,
+                convergence_dT=3.0, mmr=mmr[m])
+        floor = grid_floor(osp, ou, od, psp, pu, pd)
+        assert_grid_parity(out["spectra"][m], osp, ups[m], ou, downs[m], od, f"atmosphere {m}",
+                           floor)
 
 
 def test_batched_mfma_contraction_tiles_and_padding(fa):
@@ -119,9 +126,24 @@ def test_batched_emission_spectra_over_grids(fa):
         gr.load_opacities(opacities=op)
         grids.append(gr)
     res = fa.batched_emission_spectra(grids, n_timesteps=30)
+    tabs_o = {"1H2-16O": O.Table(op["1H2-16O"].values, op["1H2-16O"].pressure,
+                                 op["1H2-16O"].temperature)}
     for gr, (spec, T, it) in zip(grids, res):
         s1, T1, th1, _ = gr.emission_spectrum(n_timesteps=30)
         gr._close_engine()
         assert it == th1.shape[1] // 2
-        assert rel(T, T1) < 1e-10
-        assert rel(spec.flux, s1.flux) < 1e-10
+        # batch (K7 MFMA contraction) and single (K3) round the species sum differently; both
+        # must sit within the reference's own one-ulp floor of the oracle's T and spectrum
+        pl = gr.planet
+        Ft = O.F_TOA(lam, T_star=pl.T_star, a_rstar=pl.a_rstar)
+
+        def run():
+            return O.emission_spectrum(tabs_o, gr.init_temperatures, gr.pressures, lam, Ft, pl.g,
+                                       pl.m_bar, pl.alpha, n_timesteps=30)
+        osp, oT, *_ = run()
+        with perturbed_exp():
+            psp, pT, *_ = run()
+        fT, fS = rel(pT, oT), rel(psp, osp)
+        for t, sp_ in ((T, spec.flux), (T1, s1.flux)):
+            assert rel(t, oT) <= max(1e-10, 2 * fT), (rel(t, oT), fT)
+            assert rel(sp_, osp) <= max(1e-10, 2 * fS), (rel(sp_, osp), fS)

@@ -5,7 +5,8 @@ import numpy as np
 import pytest
 
 from oracle import frei_oracle as O
-from tests.parity import EPS, assert_flux_parity, assert_grid_parity, rel, row_normwise
+from tests.parity import (EPS, assert_flux_parity, assert_grid_parity, grid_floor,
+                          perturbed_exp, rel, row_normwise)
 
 pytestmark = pytest.mark.gpu
 
@@ -22,6 +23,20 @@ def fa():
 
 def _cond(shape):
     return dict(up=np.zeros(shape), down=np.zeros(shape), delta=1.0)
+
+
+def _floor(run, ref=None):
+    """One-ulp floor of an oracle run (``run()`` -> O.emission_spectrum's tuple): its outputs
+    with exp / expm1 one ulp off, against the unperturbed run; with ``ref`` (the reference's
+    (spectrum, F_up, F_down)) also the oracle's own distance to the reference."""
+    o = run()
+    with perturbed_exp():
+        p = run()
+    f = grid_floor(o[0], o[4], o[5], p[0], p[4], p[5])
+    if ref is not None:
+        f = tuple(max(a, b) for a, b in zip(f, grid_floor(ref[0], ref[1], ref[2], o[0], o[4],
+                                                         o[5])))
+    return f
 
 
 def test_propagate_fluxes_matches_reference(fa, golden):
@@ -269,8 +284,12 @@ def _grid_run(fa, C, pre, tabs_f, tabs_o, lam, p, T0, n, Ft=None):
     up, down = grid.engine().get_fluxes()
     assert_flux_parity(up, C[pre + "F_up"], cond["up"], delta, pre + "F_up")
     assert_flux_parity(down, C[pre + "F_down"], cond["down"], delta, pre + "F_down")
+    floor = _floor(lambda: O.emission_spectrum(tabs_o, T0, p, lam,
+                                               O.F_TOA(lam) if Ft is None else Ft, G_J, M_BAR,
+                                               1, n_timesteps=n),
+                   (C[pre + "spectrum"], C[pre + "F_up"], C[pre + "F_down"]))
     assert_grid_parity(spec.flux, C[pre + "spectrum"], up, C[pre + "F_up"], down,
-                       C[pre + "F_down"], pre + " vs reference")
+                       C[pre + "F_down"], pre + " vs reference", floor)
     return grid, spec, T, dtaus
 
 
@@ -345,7 +364,10 @@ def test_eight_species_device_tables_match_oracle(fa):
     up, down = grid.engine().get_fluxes()
     assert_flux_parity(up, ou, cond["up"], delta, "F_up")
     assert_flux_parity(down, od, cond["down"], delta, "F_down")
-    assert_grid_parity(spec.flux, osp, up, ou, down, od, "8 species")
+    floor = _floor(lambda: O.emission_spectrum(
+        tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1, n_timesteps=2,
+        n_zero_crossings=10**6, convergence_dT=-1, mmr=mmr))
+    assert_grid_parity(spec.flux, osp, up, ou, down, od, "8 species", floor)
     assert row_normwise(dtaus, odt) < 1e-10
 
 
@@ -377,7 +399,9 @@ def test_nan_in_table_is_skipped_like_xarray_sum(fa):
     assert relT < 1e-10 and np.all(np.isfinite(spec.flux))
     assert_flux_parity(spec.flux, osp, cond["up"][-1], max(EPS, relT), "spectrum with NaN band")
     up, down = grid.engine().get_fluxes()
-    assert_grid_parity(spec.flux, osp, up, ou, down, od, "NaN band")
+    floor = _floor(lambda: O.emission_spectrum(tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1,
+                                               n_timesteps=2))
+    assert_grid_parity(spec.flux, osp, up, ou, down, od, "NaN band", floor)
 
 
 @pytest.mark.parametrize("mode", ["single_T", "offnode_p", "mixed_T"])
@@ -417,7 +441,9 @@ def test_generic_sweep_path_matches_oracle(fa, mode):
     up, down = grid.engine().get_fluxes()
     assert_flux_parity(up, ou, cond["up"], delta, mode + " F_up")
     assert_flux_parity(down, od, cond["down"], delta, mode + " F_down")
-    assert_grid_parity(spec.flux, osp, up, ou, down, od, mode)
+    floor = _floor(lambda: O.emission_spectrum(tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1,
+                                               n_timesteps=3))
+    assert_grid_parity(spec.flux, osp, up, ou, down, od, mode, floor)
     assert row_normwise(dtaus, odt) < 1e-10
 
 
@@ -454,6 +480,9 @@ def test_species_contraction_matches_per_species_sum(fa, monkeypatch):
     osp, oT, oth, odt, ou, od, it = O.emission_spectrum(
         tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1, n_timesteps=3,
         n_zero_crossings=10 ** 6, convergence_dT=-1, mmr=mmr, err=cond)
+    floor = _floor(lambda: O.emission_spectrum(
+        tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1, n_timesteps=3,
+        n_zero_crossings=10 ** 6, convergence_dT=-1, mmr=mmr))
     for mode in ("1", "0"):
         relT = rel(out[mode]["final_T"], oT)
         assert relT < 1e-10
@@ -463,7 +492,7 @@ def test_species_contraction_matches_per_species_sum(fa, monkeypatch):
         assert_flux_parity(up, ou, cond["up"], delta, "F_up " + mode)
         assert_flux_parity(down, od, cond["down"], delta, "F_down " + mode)
         assert_grid_parity(out[mode]["spectrum"], osp, up, ou, down, od,
-                           "contracted" if mode == "1" else "per-species")
+                           "contracted" if mode == "1" else "per-species", floor)
 
 
 @pytest.mark.parametrize("red_mode", ["stage", "rows", "full"])   # partial-sum layouts
