@@ -7,7 +7,7 @@ species-summed opacity assembly, radiative-equilibrium T-P loop): the public nam
 """
 from .batch import BatchEngine, batched_emission_spectra
 from .binning import BinnedTable, CrossSection, open_cross_section
-from .chemistry import chemistry, iso_to_mass, iso_to_species
+from .chemistry import ChemistryTable, chemistry, iso_to_mass, iso_to_species
 from .core import (B_star, F_TOA, Grid, Planet, Spectrum, contribution_function,
                    effective_temperature,
                    effective_temperature_milne, effective_temperature_planck, wavelength_grid)
@@ -25,4 +25,4 @@ __all__ = ["Planet", "Grid", "Spectrum", "effective_temperature", "wavelength_gr
            "iso_to_mass", "pressure_grid", "temperature_grid", "propagate_fluxes", "emit",
            "absorb", "BB", "E", "Engine", "partition", "trapz_weights", "CrossSection",
            "BinnedTable", "open_cross_section", "contribution_function", "BatchEngine",
-           "batched_emission_spectra"]
+           "batched_emission_spectra", "ChemistryTable"]

@@ -45,6 +45,7 @@ SIGNATURES = {
                                                 ctypes.c_double, ctypes.c_double, _dp,
                                                 ctypes.c_int, _dp, ctypes.c_int]),
     "frei_set_mmr": (ctypes.c_int, [_vp, _dp]),
+    "frei_set_chemistry": (ctypes.c_int, [_vp, _dp, _dp, ctypes.c_int, _dp, ctypes.c_int]),
     "frei_set_fluxes": (ctypes.c_int, [_vp, _dp, _dp]),
     "frei_get_fluxes": (ctypes.c_int, [_vp, _dp, _dp]),
     "frei_set_temperatures": (ctypes.c_int, [_vp, _dp]),

@@ -4,7 +4,10 @@ FastChem (``pyfastchem``, third-party C++, unpinned) is not part of this engine;
 reference when pyfastchem is absent (chemistry.py:142-153) the built-in mock is used:
 every species has VMR = 1.5e-3 (chemistry.py:243), mmr = VMR * mass / m_bar.  The
 engine takes per-layer mmr arrays, so a real chemistry provider can be plugged in by
-passing ``mmr=`` to :class:`frei_amd.engine.Engine` / ``Grid.load_opacities``.
+passing ``mmr=`` to :class:`frei_amd.engine.Engine` / ``Grid.load_opacities``; a provider
+whose abundances depend on temperature (FastChem's equilibrium chemistry) is passed as a
+:class:`ChemistryTable` — its output tabulated on (T, p) nodes — and the device re-evaluates
+every layer's mmr at the layer's current temperature each sweep (frei_set_chemistry).
 """
 import re
 
@@ -13,7 +16,7 @@ import numpy as np
 from .constants import AMU, M_BAR_DEFAULT
 from .units import value
 
-__all__ = ["chemistry", "iso_to_species", "iso_to_mass"]
+__all__ = ["chemistry", "iso_to_species", "iso_to_mass", "ChemistryTable"]
 
 MOCK_VMR = 1.5e-3
 
@@ -62,3 +65,30 @@ def chemistry(temperatures, pressures, species, return_vmr=False, m_bar=M_BAR_DE
     if return_vmr:
         return mmr, vmr
     return mmr
+
+
+class ChemistryTable:
+    """Mass mixing ratios tabulated on (temperature, pressure) nodes, e.g. a FastChem run
+    over a (T, p) grid: ``values`` is ``{species: array[n_T][n_p]}`` (or an array
+    [n_species][n_T][n_p] in the opacity dict's species order), ``temperature`` in K and
+    ``pressure`` in bar, both ascending.  The engine interpolates it at each layer's
+    (T, p) every sweep — linear in T and in log10 p, clamped to the node range — the way the
+    reference calls ``chemistry(T, p)`` inside every ``kappa`` (opacity.py:246-248)."""
+
+    def __init__(self, values, temperature, pressure):
+        self.temperature = np.asarray(value(temperature, "K"), dtype=np.float64)
+        self.pressure = np.asarray(value(pressure, "bar"), dtype=np.float64)
+        self.values = values
+        if np.any(np.diff(self.temperature) <= 0) or np.any(np.diff(self.pressure) <= 0):
+            raise ValueError("ChemistryTable nodes must be strictly ascending")
+
+    def array(self, species):
+        """[n_species][n_T][n_p] in the order of ``species``."""
+        if isinstance(self.values, dict):
+            v = np.array([np.asarray(self.values[n], dtype=np.float64) for n in species])
+        else:
+            v = np.asarray(self.values, dtype=np.float64)
+        shape = (len(species), self.temperature.size, self.pressure.size)
+        if v.shape != shape:
+            raise ValueError(f"chemistry table must be {shape}, got {v.shape}")
+        return np.ascontiguousarray(v)

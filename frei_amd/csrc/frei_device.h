@@ -183,7 +183,52 @@ struct AtmStride {
   const double* g;   // per-atmosphere gravity (nullptr: SetupArgs.g)
 };
 
+// Temperature-dependent chemistry (the reference calls chemistry(T, p) inside every kappa,
+// opacity.py:246-248): mass mixing ratios tabulated on (T, p) nodes, interpolated at each
+// sweep step's layer (T_i, p_i) when the update kernel writes the next sweep's step table —
+// linear in T and in log10 p, clamped to the node range.  tab == nullptr: the fixed
+// per-layer mmr arrays of frei_set_mmr.
+struct ChemArgs {
+  const double* tab;       // [n_species][n_T][n_p]
+  const double* T;         // [n_T] ascending (K)
+  const int32_t* pj;       // [n_layers] pressure bracket of each layer (node index)
+  const double* pz;        // [n_layers] weight of node pj + 1 (log10 p)
+  int n_T, n_p;
+};
+
+// Bracket of x on ascending nodes g[n] clamped to [g0, g_{n-1}]: node i <= n - 2 and the
+// weight y of node i + 1 (0 when n == 1).
+__host__ __device__ inline void chem_bracket(const double* g, int n, double x, int& i,
+                                             double& y) {
+  i = 0;
+  y = 0.0;
+  if (n < 2) return;
+  const double xc = x < g[0] ? g[0] : (x > g[n - 1] ? g[n - 1] : x);
+  int lo = 0, hi = n - 2;   // largest i in [0, n-2] with g[i] <= xc
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (g[mid] <= xc) lo = mid; else hi = mid - 1;
+  }
+  i = lo;
+  y = (xc - g[i]) / (g[i + 1] - g[i]);
+}
+
+// mmr of species s at layer i (pressure bracket pj[i], pz[i]) and temperature T:
+// ((v00 (1 - z) + v01 z) (1 - y) + (v10 (1 - z) + v11 z) y), exact order (oracle/frei_oracle.py
+// ChemistryTable restates it).
+__host__ __device__ inline double chem_mmr_at(const ChemArgs& c, int s, int j, double z,
+                                              double T) {
+  int it;
+  double y;
+  chem_bracket(c.T, c.n_T, T, it, y);
+  const double* v = c.tab + ((int64_t)s * c.n_T + it) * c.n_p;
+  auto row = [&](const double* r) { return c.n_p > 1 ? r[j] * (1.0 - z) + r[j + 1] * z : r[0]; };
+  const double a = row(v);
+  return c.n_T > 1 ? a * (1.0 - y) + row(v + c.n_p) * y : a;
+}
+
 struct SetupArgs {
+  ChemArgs chem;           // T-dependent chemistry (chem.tab == nullptr: fixed mmr)
   int n_layers, n_species, fast;
   int n_tnodes;            // total sorted T nodes over species (tnodes length)
   double* T;               // device temperatures [n_layers]

@@ -1076,6 +1076,12 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
   const int nL = u.n_layers;
   const int ns = nL - 1;
   const int nS = u.n_species;
+  // mixing ratio of species s at layer i: the chemistry table at the layer's current T
+  // (kappa's chemistry(T, p) call, opacity.py:246-248), else the fixed per-layer arrays
+  auto MMR = [&](int s, int i) {
+    return u.chem.tab ? chem_mmr_at(u.chem, s, u.chem.pj[i], u.chem.pz[i], T[i])
+                      : mmr[(int64_t)s * nL + i];
+  };
   if (u.fast && u.shared) {
     for (int k = threadIdx.x; k < ns; k += blockDim.x) {
       const int i = step_layer(dir, k, nL);
@@ -1093,7 +1099,7 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
       f->off = off;
       f->wlo = wlo;
       f->whi = whi;
-      for (int s = 0; s < kMaxFastS; ++s) f->mmr[s] = s < nS ? mmr[(int64_t)s * nL + i] : 0.0;
+      for (int s = 0; s < kMaxFastS; ++s) f->mmr[s] = s < nS ? MMR(s, i) : 0.0;
     }
     return;
   }
@@ -1124,7 +1130,7 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
       f->off[s] = off;
       f->wlo[s] = wlo;
       f->whi[s] = whi;
-      f->mmr[s] = mmr[(int64_t)s * nL + i];
+      f->mmr[s] = MMR(s, i);
     }
     return;
   }
@@ -1143,8 +1149,8 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
   for (int idx = threadIdx.x; idx < ns * nS; idx += blockDim.x) {
     const int k = idx / nS, s = idx % nS;
     const int i = step_layer(dir, k, nL);
-    u.terms[idx] = make_term(spec[s], pmeta[(int64_t)s * nL + i], tnodes, u.tperm,
-                             mmr[(int64_t)s * nL + i], T[i], u.fast);
+    u.terms[idx] = make_term(spec[s], pmeta[(int64_t)s * nL + i], tnodes, u.tperm, MMR(s, i),
+                             T[i], u.fast);
   }
 }
 

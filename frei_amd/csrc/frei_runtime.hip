@@ -174,6 +174,12 @@ struct frei_ctx {
   size_t lds_per_block = 64 * 1024;     // hipDeviceProp sharedMemPerBlock
   bool ftoa_per_atm = false;            // batched: one F_TOA per atmosphere (frei_set_ftoa_batch)
   double setup_ms[5] = {0, 0, 0, 0, 0};  // last metadata build, by phase (frei_setup_timing)
+  // T-dependent chemistry (frei_set_chemistry): mmr tables on (T, p) nodes
+  bool chem_on = false;
+  int chem_nT = 0, chem_np = 0;
+  std::vector<double> chem_tab, chem_T, chem_logp;   // host copies (frei_kappa)
+  double *d_chem_tab = nullptr, *d_chem_T = nullptr, *d_chem_pz = nullptr;
+  int32_t* d_chem_pj = nullptr;
   // P2P exchange over xGMI (frei_comm_p2p_*): own mailbox (uncached device memory), the
   // mapped mailboxes of every rank (own included) and the per-sweep sequence number
   double* d_mbox = nullptr;
@@ -226,7 +232,8 @@ template <typename Lap>
 int build_contracted(frei_ctx* c, bool shared_fast, Lap&& lap) {
   const int nL = c->nL, S = c->S;
   const bool batch = c->n_atm > 1;
-  bool on = shared_fast && (S >= 2 || batch) && (c->eff_mode != 0 || batch);
+  // (a T-dependent chemistry changes mmr every sweep: the species sum stays in the sweep)
+  bool on = shared_fast && (S >= 2 || batch) && (c->eff_mode != 0 || batch) && !c->chem_on;
   for (int s = 0; s < S && on; ++s) on = !c->sp[s].has_nan;
   std::vector<int32_t> prow(nL, 0);
   if (on) {
@@ -440,6 +447,14 @@ SetupArgs setup_args(frei_ctx* c) {
   u.ssteps = c->d_ssteps;
   u.shared = c->shared;
   u.bs = atm_stride(c);
+  if (c->chem_on) {
+    u.chem.tab = c->d_chem_tab;
+    u.chem.T = c->d_chem_T;
+    u.chem.pj = c->d_chem_pj;
+    u.chem.pz = c->d_chem_pz;
+    u.chem.n_T = c->chem_nT;
+    u.chem.n_p = c->chem_np;
+  }
   return u;
 }
 
@@ -825,6 +840,10 @@ int frei_ctx_destroy(frei_ctx* c) {
   for (auto& s : c->sp) dfree(s.d_tab);
   dfree(c->d_eff);
   dfree(c->d_smeta_eff);
+  dfree(c->d_chem_tab);
+  dfree(c->d_chem_T);
+  dfree(c->d_chem_pz);
+  dfree(c->d_chem_pj);
   dfree(c->d_ones);
   dfree(c->d_prow);
   double* dd[] = {c->d_c1, c->d_lk, c->d_sig, c->d_ftoa, c->d_wtr, c->d_p, c->d_lnp,
@@ -1025,6 +1044,53 @@ int frei_set_ftoa_batch(frei_ctx* c, const double* f_toa) {
   dfree(c->d_ftoa);
   c->d_ftoa = d;
   c->ftoa_per_atm = true;
+  return 0;
+}
+
+int frei_set_chemistry(frei_ctx* c, const double* values, const double* T_nodes, int n_T,
+                       const double* p_nodes, int n_p) {
+  if (!c) return fail("null argument");
+  if (!c->grid_set) return fail("frei_set_grid must be called first");
+  TRY(set_device(c));
+  if (!values) {   // back to the fixed per-layer mmr arrays
+    c->chem_on = false;
+    c->meta_dirty = true;
+    return 0;
+  }
+  if (c->n_atm > 1) return fail("a chemistry table is per atmosphere: not for batched contexts");
+  if (!T_nodes || !p_nodes || n_T < 1 || n_p < 1) return fail("chemistry table needs nodes");
+  for (int k = 1; k < n_T; ++k)
+    if (!(T_nodes[k] > T_nodes[k - 1])) return fail("chemistry T nodes must ascend");
+  for (int k = 0; k < n_p; ++k)
+    if (!(p_nodes[k] > 0) || (k > 0 && !(p_nodes[k] > p_nodes[k - 1])))
+      return fail("chemistry p nodes must be positive and ascend");
+  const int nL = c->nL;
+  const size_t nv = (size_t)c->S * n_T * n_p;
+  c->chem_tab.assign(values, values + nv);
+  c->chem_T.assign(T_nodes, T_nodes + n_T);
+  c->chem_logp.resize(n_p);
+  for (int k = 0; k < n_p; ++k) c->chem_logp[k] = std::log10(p_nodes[k]);
+  std::vector<int32_t> pj(nL);
+  std::vector<double> pz(nL);
+  for (int l = 0; l < nL; ++l)   // layer pressures are fixed: their log10 p brackets once
+    chem_bracket(c->chem_logp.data(), n_p, std::log10(c->p[l]), pj[l], pz[l]);
+  dfree(c->d_chem_tab);
+  dfree(c->d_chem_T);
+  dfree(c->d_chem_pj);
+  dfree(c->d_chem_pz);
+  TRY(dalloc(&c->d_chem_tab, nv));
+  TRY(dalloc(&c->d_chem_T, n_T));
+  TRY(dalloc(&c->d_chem_pj, nL));
+  TRY(dalloc(&c->d_chem_pz, nL));
+  TRY(h2d(c->d_chem_tab, c->chem_tab.data(), nv, c->stream));
+  TRY(h2d(c->d_chem_T, c->chem_T.data(), n_T, c->stream));
+  TRY(h2d(c->d_chem_pj, pj.data(), nL, c->stream));
+  TRY(h2d(c->d_chem_pz, pz.data(), nL, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->chem_nT = n_T;
+  c->chem_np = n_p;
+  c->chem_on = true;
+  c->meta_dirty = true;   // the species contraction (K3) no longer applies
   return 0;
 }
 
@@ -1302,10 +1368,18 @@ int frei_kappa(frei_ctx* c, double T, double p, double* k, double* sigma) {
       pm.wp_hi = y;
       pm.oob = oob;
     }
-    // mmr: the layer whose pressure equals p, else the first layer's value
+    // mmr: the chemistry table at (T, p) when set (opacity.py:246-248), else the layer whose
+    // pressure equals p, else the first layer's value
     double m = c->mmr[(size_t)s * c->nL];
     for (int l = 0; l < c->nL; ++l)
       if (c->p[l] == p) m = c->mmr[(size_t)s * c->nL + l];
+    if (c->chem_on) {
+      int j;
+      double z;
+      chem_bracket(c->chem_logp.data(), c->chem_np, std::log10(p), j, z);
+      ChemArgs h{c->chem_tab.data(), c->chem_T.data(), nullptr, nullptr, c->chem_nT, c->chem_np};
+      m = chem_mmr_at(h, s, j, z, T);
+    }
     terms[s] = make_term(sm, pm, c->tnodes.data(), c->tperm.data(), m, T, 0);
   }
   TermP* d_terms = nullptr;

@@ -13,7 +13,7 @@ import numpy as np
 
 from . import _native as N
 from .binning import BinnedTable
-from .chemistry import chemistry
+from .chemistry import ChemistryTable, chemistry
 from .constants import BAR, C, H, K_B, M_BAR_DEFAULT, UM
 from .opacity import SeparableTable, sigma_scattering
 from .units import scalar, value
@@ -65,7 +65,8 @@ class Engine:
     Parameters mirror the reference's Grid/Planet: ``p_bar`` layer pressures (bar,
     descending), ``opacities`` dict of tables, ``g`` (cm s^-2), ``m_bar`` (g),
     ``F_toa`` (erg s^-1 cm^-3, global grid) and ``mmr`` [n_species][n_layers]
-    (default: the reference's mock chemistry, chemistry.py:207-246).
+    (default: the reference's mock chemistry, chemistry.py:207-246) or a
+    :class:`~frei_amd.chemistry.ChemistryTable` (T-dependent, re-evaluated every sweep).
     """
 
     def __init__(self, lam_um, p_bar, opacities, g=2478.6519476149147, m_bar=M_BAR_DEFAULT,
@@ -100,13 +101,21 @@ class Engine:
                                   self.g, self.m_bar))
         for s, name in enumerate(self.names):
             self._set_table(s, opacities[name], sl)
-        if mmr is None:
+        chem = mmr if isinstance(mmr, ChemistryTable) else None
+        if mmr is None or chem is not None:
             T0 = np.full(self.n_layers, 1000.0)
             mm = chemistry(T0, self.p_bar, self.names, m_bar=self.m_bar)
             mmr = np.array([mm[nm] for nm in self.names])
         self.mmr = N.f64(np.broadcast_to(np.asarray(mmr, dtype=float),
                                          (len(self.names), self.n_layers)))
         N.check(lib.frei_set_mmr(ctx, N.dptr(self.mmr)))
+        self.chemistry = chem
+        if chem is not None:   # T-dependent chemistry, re-evaluated on the device every sweep
+            v = N.f64(chem.array(self.names))
+            N.check(lib.frei_set_chemistry(ctx, N.dptr(v), N.dptr(N.f64(chem.temperature)),
+                                           chem.temperature.size,
+                                           N.dptr(N.f64(chem.pressure * BAR)),
+                                           chem.pressure.size))
         self._ag_keep = None
         if comm is not None:
             self._join(comm)

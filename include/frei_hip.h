@@ -109,6 +109,18 @@ int frei_set_table_separable(frei_ctx* ctx, int s, const double* base, const dou
  * the reference's mock gives a constant VMR).  CIA-like tables take their weights here. */
 int frei_set_mmr(frei_ctx* ctx, const double* mmr);
 
+/*
+ * Temperature-dependent chemistry (chemistry(T, p) inside every kappa call,
+ * opacity.py:246-248; chemistry.py:114-205): mass mixing ratios values[n_species][n_T][n_p]
+ * on ascending T_nodes (K) x p_nodes (dyn cm^-2).  At every sweep step the layer's mmr is
+ * interpolated at its current (T_i, p_i) — linear in T and in log10 p, clamped to the nodes —
+ * when the update kernel writes the next sweep's step table; the species sum then stays in
+ * the sweep (no K3 contraction).  values = NULL returns to frei_set_mmr's fixed arrays.
+ * Single-atmosphere contexts; call after frei_set_grid.
+ */
+int frei_set_chemistry(frei_ctx* ctx, const double* values, const double* T_nodes, int n_T,
+                       const double* p_nodes, int n_p);
+
 /* Flux state [n_layers][n_lam] (this slice), caller layout row-major. */
 int frei_set_fluxes(frei_ctx* ctx, const double* up, const double* down);
 int frei_get_fluxes(frei_ctx* ctx, double* up, double* down);

@@ -337,7 +337,7 @@ def _sweep(direction, tables, T, p_bar, lam_um, F_toa, g, m_bar, alpha, F_up, F_
         else:
             p2b, T2 = p_bar[i + 1], T[i + 1]
         p1b, T1 = p_bar[i], T[i]
-        k, sigma = kappa(tables, T1, p1b, lam_um, m_bar, mmr=mmr_fn(i))
+        k, sigma = kappa(tables, T1, p1b, lam_um, m_bar, mmr=mmr_fn(i, T1, p1b))
         p1, p2 = p1b * BAR, p2b * BAR
         dtau = (p1 - p2) / g * k
         dtaus.append(dtau)
@@ -366,13 +366,51 @@ def _sweep(direction, tables, T, p_bar, lam_um, F_toa, g, m_bar, alpha, F_up, F_
     return F_up, F_down, T - dT, np.array(dtaus), dT
 
 
+class ChemistryTable:
+    """Mass mixing ratios on (T, p) nodes, values[S][n_T][n_p], T (K) and p (bar) ascending:
+    the checker of the engine's frei_set_chemistry interface (no reference counterpart: the
+    reference calls FastChem, chemistry.py:114-205, at every kappa; parity against FastChem is
+    unpinned).  Linear in T and in log10 p (p in dyn cm^-2, as the engine receives it),
+    clamped to the nodes, in the engine's exact operation order
+    ((v00 (1 - z) + v01 z) (1 - y) + (v10 (1 - z) + v11 z) y)."""
+
+    def __init__(self, values, T_nodes, p_nodes_bar):
+        self.values = np.asarray(values, dtype=float)
+        self.T = np.asarray(T_nodes, dtype=float)
+        self.logp = np.log10(np.asarray(p_nodes_bar, dtype=float) * BAR)
+
+    @staticmethod
+    def _bracket(g, x):
+        if g.size < 2:
+            return 0, 0.0
+        xc = min(max(x, g[0]), g[-1])
+        i = int(min(np.searchsorted(g, xc, side="right") - 1, g.size - 2))
+        return i, (xc - g[i]) / (g[i + 1] - g[i])
+
+    def __call__(self, T, p_bar):
+        it, y = self._bracket(self.T, float(T))
+        j, z = self._bracket(self.logp, float(np.log10(p_bar * BAR)))
+        out = np.empty(self.values.shape[0])
+        for s in range(out.size):
+            def row(k):
+                r = self.values[s, k]
+                return r[j] * (1.0 - z) + r[j + 1] * z if r.size > 1 else r[0]
+            a = row(it)
+            out[s] = a * (1.0 - y) + row(it + 1) * y if self.T.size > 1 else a
+        return out
+
+
 def _mmr_fn(tables, m_bar, mmr):
+    """mmr of every species at layer i, temperature T, pressure p (bar): the mock, a fixed
+    [S][n_layers] array, or a ChemistryTable evaluated at (T, p) (opacity.py:246-248)."""
     names = list(tables)
     if mmr is None:
         m = mock_mmr(names, m_bar)
-        return lambda i: m
+        return lambda i, T, p: m
+    if callable(mmr):
+        return lambda i, T, p: mmr(T, p)
     mmr = np.asarray(mmr, dtype=float)
-    return lambda i: mmr[:, i]
+    return lambda i, T, p: mmr[:, i]
 
 
 def emit(tables, T, p_bar, lam_um, F_toa, g, m_bar, alpha=1, fluxes_up=None,

@@ -576,3 +576,75 @@ def test_shims_reuse_device_context_and_vector_kappa(fa, golden):
     assert k1.shape == (s["lam"].size,)               # one point: flat, like the reference
     E.clear_engine_cache()
     assert not E._ENGINE_CACHE and eng._ctx is None
+
+
+def _chem_table(names, T_lo=300.0, T_hi=4000.0, n_T=14, n_p=9):
+    """Synthetic equilibrium-like chemistry: H2O falls and CO rises with T (log-space tanh
+    around 1500 K), weak pressure dependence; mass mixing ratios on (T, log p) nodes."""
+    T = np.linspace(T_lo, T_hi, n_T)
+    p = np.logspace(-7, 3, n_p)
+    x = np.tanh((T[:, None] - 1500.0) / 400.0) + 0.05 * np.log10(p)[None, :]
+    base = O.mock_mmr(names, M_BAR)
+    vals = []
+    for s, n in enumerate(names):
+        sign = -1.0 if s % 2 == 0 else 1.0
+        vals.append(base[s] * 10 ** (0.8 * sign * x))
+    return np.array(vals), T, p
+
+
+@pytest.mark.parametrize("case", ["c1", "c2_like"])
+def test_temperature_dependent_chemistry_matches_oracle(fa, case):
+    """A chemistry table (mmr on (T, p) nodes, re-interpolated at every layer's current T each
+    sweep, like the reference's chemistry(T, p) call inside kappa, opacity.py:246-248): the
+    sweep keeps the per-species sum (no K3), and the T-P loop matches the oracle given the same
+    table (parity against FastChem itself is unpinned: it is third-party)."""
+    rng = np.random.default_rng(41)
+    if case == "c1":
+        lam, _, _ = O.wavelength_grid(0.5, 10, 500)
+        p = O.pressure_grid(30, -6, np.log10(200))
+        T0 = O.temperature_grid(p, 2400.0, 0.1, 0.1)
+        n_it, nzc, thr = 60, 2, 3.0
+    else:
+        lam, _, _ = O.wavelength_grid(0.5, 10, 2048)
+        p = O.pressure_grid(60, -6, np.log10(200))
+        T0 = O.temperature_grid(p, 1500.0, 0.1, 0.1)
+        n_it, nzc, thr = 3, 10 ** 6, -1.0
+    names = ["1H2-16O", "12C-16O", "12C-1H4"]
+    Tn = np.linspace(0.7 * T0.min(), 1.3 * T0.max(), 10)
+    tabs_o, tabs_f = {}, {}
+    for n in names:
+        base = 10 ** rng.uniform(-3, 1, lam.size)
+        fp, fT = (p / 1.0) ** 0.1, (Tn / 1000.0) ** 0.5
+        tabs_o[n] = O.Table(O.separable_table(base, fp, fT), p, Tn)
+        tabs_f[n] = fa.SeparableTable(base, fp, fT, p, Tn)
+    vals, cT, cp = _chem_table(names)
+    chem_f = fa.ChemistryTable({n: vals[s] for s, n in enumerate(names)}, cT, cp)
+    chem_o = O.ChemistryTable(vals, cT, cp)
+    eng = fa.Engine(lam, p, tabs_f, mmr=chem_f)
+    try:
+        assert not eng.path()["contracted"]
+        out = eng.run(T0, n_timesteps=n_it, n_zero_crossings=nzc, convergence_dT=thr)
+        up, down = eng.get_fluxes()
+        # kappa at arbitrary (T, p): mmr from the table at that point
+        for Tq, pq in ((T0[3] * 1.1, p[3]), (T0[-5], np.sqrt(p[7] * p[8]))):
+            k, _ = eng.kappa(Tq, pq)
+            ko, _ = O.kappa(tabs_o, Tq, pq, lam, M_BAR, mmr=chem_o(Tq, pq))
+            assert rel(k, ko) < 1e-13
+    finally:
+        eng.close()
+
+    def run():
+        return O.emission_spectrum(tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1,
+                                   n_timesteps=n_it, n_zero_crossings=nzc, convergence_dT=thr,
+                                   mmr=chem_o)
+    osp, oT, oth, odt, ou, od, it = run()
+    assert out["n_iter"] == it
+    with perturbed_exp():
+        psp, pT, _, _, pu, pd, _ = run()
+    assert rel(out["final_T"], oT) <= max(1e-10, 2 * rel(pT, oT))
+    assert_grid_parity(out["spectrum"], osp, up, ou, down, od, "chemistry " + case,
+                       grid_floor(osp, ou, od, psp, pu, pd))
+    # the chemistry really moved with T: mmr at the final vs the initial profile
+    m0 = np.array([chem_o(t, pb) for t, pb in zip(T0, p)])
+    m1 = np.array([chem_o(t, pb) for t, pb in zip(out["final_T"], p)])
+    assert np.max(np.abs(m1 - m0) / m0) > 1e-3

@@ -96,3 +96,25 @@ def test_build_script_lists_every_hip_source():
     here = os.path.join(os.path.dirname(build.__file__), "csrc")
     hips = sorted(f for f in os.listdir(here) if f.endswith(".hip"))
     assert sorted(os.path.basename(s) for s in build.SOURCES) == hips
+
+
+def test_chemistry_table_interpolation_contract():
+    """The ChemistryTable interface (engine: frei_set_chemistry; checker:
+    oracle.ChemistryTable): exact at nodes, linear in T and log10 p between them, clamped
+    outside; the host wrapper orders species like the opacity dict."""
+    import numpy as np
+    import frei_amd as fa
+    from oracle import frei_oracle as O
+    T = np.array([500.0, 1000.0, 2000.0])
+    p = np.array([1e-4, 1e-2, 1.0, 100.0])
+    vals = np.arange(2 * 3 * 4, dtype=float).reshape(2, 3, 4) + 1.0
+    c = O.ChemistryTable(vals, T, p)
+    for i, t in enumerate(T):
+        for j, pb in enumerate(p):
+            assert np.allclose(c(t, pb), vals[:, i, j], rtol=1e-14, atol=0)
+    mid = c(750.0, 1e-3)     # halfway in T and in log10 p
+    assert np.allclose(mid, vals[:, :2, :2].mean(axis=(1, 2)), rtol=1e-12)
+    assert np.array_equal(c(10.0, 1e-9), vals[:, 0, 0])      # clamped below
+    assert np.array_equal(c(9e3, 1e5), vals[:, -1, -1])     # clamped above
+    t = fa.ChemistryTable({"12C-16O": vals[1], "1H2-16O": vals[0]}, T, p)
+    assert np.array_equal(t.array(["1H2-16O", "12C-16O"]), vals)
