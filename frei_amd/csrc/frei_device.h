@@ -264,6 +264,7 @@ struct FastArgs {
   AtmStride bs;            // batched atmospheres (blockIdx.y of the sweep kernels)
   int n_atm;               // atmospheres in the launch (0 or 1: a single atmosphere)
   int red_rows;            // one-lane sweep: per-row partial sums in LDS (fits: few layers)
+  int unit_mmr;            // S = 1 with mmr = 1 everywhere (the contracted table, K3)
 };
 
 struct SweepArgs {

@@ -35,10 +35,16 @@ __device__ __forceinline__ double planck(double c1, double lk, double T) {
 #ifndef FREI_EXPM1_VREG
 #define FREI_EXPM1_VREG 1
 #endif
-// The sweeps' Planck values: expm1 coefficients in VGPRs (fm::Expm1Reg, loaded once).
+// The sweeps' Planck values: expm1 coefficients in VGPRs (fm::Expm1Reg, loaded once), the
+// range-select-free expm1 for exponents <= 600 and an IEEE fallback branch (execz-skipped)
+// for the rare lanes above — cold layers at short wavelengths, where expm1 passes 2^865 and
+// the guard-free division could lose the denormal quotient.
 __device__ __forceinline__ double planck(double c1, double lk, double T, const fm::Expm1Reg& k) {
 #if FREI_EXPM1_VREG && !defined(FREI_MEMONLY)
-  return fm::div_big(c1, fm::expm1(fm::div(kHC, lk * T), k));
+  const double x = fm::div(kHC, lk * T);
+  double B = fm::div(c1, fm::expm1_mid(x < 600.0 ? x : 600.0, k));
+  if (__builtin_expect(!(x <= 600.0), 0)) B = c1 / fm::expm1(x, k);
+  return B;
 #else
   (void)k;
   return planck(c1, lk, T);
@@ -362,11 +368,14 @@ struct StepCoef {
   int layer, top;
 };
 
-// Terms after E (twostream.py:143-176), same expression order as two_stream().
+// Terms after E (twostream.py:143-176), same expression order as two_stream().  pi_w =
+// pi (1 - w0) / (E - w0) comes from the caller; 1 / chi is formed within an ulp (it scales
+// the whole update, nothing cancels after it); the transmission's exp argument is <= 0.
 __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, double B2,
-                                          double Emw, double sq, double r, double q,
+                                          double sq, double r, double q, double pi_w,
                                           StepCoef& c) {
-  const double Tr = fm::exp((-2.0 * sq) * dtau);
+  (void)w0;
+  const double Tr = fm::exp_neg((-2.0 * sq) * dtau);
   const double zp = 0.5 * (1.0 + r);
   const double zm = 0.5 * (1.0 - r);
   const double Tr2 = Tr * Tr;
@@ -375,10 +384,9 @@ __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, dou
   const double chi = zm2 * Tr2 - zp2;
   const double xi = (zp * zm) * (1.0 - Tr2);
   const double psi = (zm2 - zp2) * Tr;
-  const double pi_w = fm::div(kPi * (1.0 - w0), Emw);
   c.psi = psi;
   c.xi = xi;
-  c.ic = fm::div(1.0, chi);
+  c.ic = fm::rcp_nr(chi);
   c.Xu = pi_w * ((B2 * (chi + xi) - psi * B1) + q * ((chi - psi) - xi));
   c.Xd = pi_w * ((B1 * (chi + xi) - psi * B2) + q * ((xi + psi) - chi));
   c.dtau = dtau;
@@ -390,17 +398,19 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
   const double E = (w0 > 0.1) ? ((1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0)) : 1.0;
   const double Emw = E - w0;
   const double q = fm::div(fm::div(B1 - B2, dtau), 2.0 * E);
-  coef_tail(w0, dtau, B1, B2, Emw, fm::sqrt(E * Emw), fm::sqrt(fm::div(Emw, E)), q, c);
+  coef_tail(w0, dtau, B1, B2, fm::sqrt(E * Emw), fm::sqrt(fm::div(Emw, E)), q,
+            fm::div(kPi * (1.0 - w0), Emw), c);
 }
 
 // Step whose w0 <= 0.1 (E = 1): E * Emw, Emw / E and Bprime / (2 E) are exact without the
 // multiply/divide and sqrt(E * Emw) == sqrt(Emw / E), so this skips two divisions and a
-// square root with bit-identical results.  Taken when the whole wave qualifies.
+// square root with bit-identical results.  pi (1 - w0) / (1 - w0) is pi within an ulp (the
+// reference's own rounding of it), so the constant replaces a third division.  Taken when
+// the whole wave qualifies.
 __device__ __forceinline__ void coef_e1(double w0, double dtau, double B1, double B2,
                                         StepCoef& c) {
-  const double Emw = 1.0 - w0;
-  const double sq = fm::sqrt(Emw);
-  coef_tail(w0, dtau, B1, B2, Emw, sq, sq, fm::div(B1 - B2, dtau) * 0.5, c);
+  const double sq = fm::sqrt(1.0 - w0);
+  coef_tail(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5, kPi, c);
 }
 
 struct PreCoef {
@@ -426,12 +436,13 @@ __host__ __device__ inline int64_t red_lds_doubles(int red_rows, int ns) {
   return (int64_t)red_rows_per_block(red_rows) * ns * 4 + (red_rows == 2 ? kStageDoubles : 0);
 }
 
-template <int DIR, int S, int PD, bool NANCHK, bool SH>
+template <int DIR, int S, int PD, bool NANCHK, bool SH, bool MM1>
 __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     FastArgs a, const FastStep* __restrict__ st, const FastStepS* __restrict__ ss,
     double* __restrict__ Fu, double* __restrict__ Fd, double* __restrict__ part,
     double* __restrict__ dtaus) {
   static_assert(PD == 1 || PD == 2 || PD == 4, "prefetch depth 1, 2 or 4");
+  static_assert(!MM1 || S == 1, "mmr = 1 only for the contracted single table");
   {  // atmosphere of a batched launch (identity for one atmosphere)
     const int m = blockIdx.y;
     Fu += m * a.bs.flux;
@@ -529,9 +540,13 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       const double vlo = v[2 * s], vhi = v[2 * s + 1];
       double ops;
       if constexpr (SH) {
-        ops = UNIV(sp[kk].mmr[s]) * ((0.0 + vlo * UNIV(sp[kk].wlo)) + vhi * UNIV(sp[kk].whi));
+        // (0 + a) + b == a + b for the non-negative table terms; the contracted table (MM1)
+        // carries mmr = 1, whose product is the identity
+        const double acc = vlo * UNIV(sp[kk].wlo) + vhi * UNIV(sp[kk].whi);
+        ops = MM1 ? acc : UNIV(sp[kk].mmr[s]) * acc;
       } else {
-        ops = st[kk].mmr[s] * ((0.0 + vlo * st[kk].wlo[s]) + vhi * st[kk].whi[s]);
+        const double acc = vlo * st[kk].wlo[s] + vhi * st[kk].whi[s];
+        ops = MM1 ? acc : st[kk].mmr[s] * acc;
       }
       // xarray nansum for S > 1 (Q8); compiled out when the tables hold no NaN (scan at load)
       if (NANCHK && S > 1) ops = isnan(ops) ? 0.0 : ops;
@@ -750,7 +765,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   // Everything group g's phase A reads, issued together one group ahead: the LDS step
   // parameters with the table rows and the stale flux (their latency overlaps).
   struct Pre {
-    double vlo, vhi, stale, wl, wh, mm, dm, T;
+    double vlo, vhi, stale, wl, wh, dm, T;
   };
   auto load = [&](int g, Pre& P) {
     const int k = clampk(Q * g + q);
@@ -758,7 +773,6 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     const double* r = tab + st.off + j;
     P.wl = st.wlo;
     P.wh = st.whi;
-    P.mm = st.mmr[0];
     P.dm = st.dm;
     P.T = DIR == kEmit ? st.T2 : st.T1;
     P.vlo = stream_load(r);
@@ -789,7 +803,8 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     const int k = Q * g + q;
     A.k = k;
     A.F_st = P.stale;
-    const double kap = P.mm * ((0.0 + P.vlo * P.wl) + P.vhi * P.wh) + sig;
+    // contracted table: mmr = 1, and (0 + a) + b == a + b for its non-negative terms
+    const double kap = (P.vlo * P.wl + P.vhi * P.wh) + sig;
     const double dm = P.dm, Tnew = P.T;
     load(g + 2, P);
     A.dtau = dm * kap;
@@ -1638,11 +1653,11 @@ void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream
   else launch_sweep_dir<kAbsorb>(a, nblocks, fast, st);
 }
 
-template <int DIR, int S, int PD, bool NC, bool SH>
+template <int DIR, int S, int PD, bool NC, bool SH, bool MM1 = false>
 static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
   const size_t shm = (size_t)red_lds_doubles(a.red_rows, a.n_steps) * sizeof(double) +
                      (SH ? (size_t)a.n_steps * sizeof(FastStepS) : 0);
-  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC, SH>),
+  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC, SH, MM1>),
                      dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1), dim3(kBlock), shm,
                      st, a, a.steps, a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
 }
@@ -1650,7 +1665,9 @@ static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
 template <int DIR, int PD, bool NC, bool SH>
 static void launch_fast_dir(int S, const FastArgs& a, int nblocks, hipStream_t st) {
   switch (S) {
-    case 1: return launch_fast_t<DIR, 1, PD, NC, SH>(a, nblocks, st);
+    case 1:
+      if (a.unit_mmr && !NC) return launch_fast_t<DIR, 1, PD, false, SH, true>(a, nblocks, st);
+      return launch_fast_t<DIR, 1, PD, NC, SH>(a, nblocks, st);
     case 2: return launch_fast_t<DIR, 2, PD, NC, SH>(a, nblocks, st);
     case 3: return launch_fast_t<DIR, 3, PD, NC, SH>(a, nblocks, st);
     case 4: return launch_fast_t<DIR, 4, PD, NC, SH>(a, nblocks, st);
@@ -1671,8 +1688,13 @@ template <bool SH>
 static void launch_fast_sh(int dir, int S, int depth, bool nan_check, const FastArgs& a,
                            int nblocks, hipStream_t st) {
   if (depth >= 4 && S == 1 && !nan_check) {  // 4 steps in flight: small slices, one table
-    if (dir == kEmit) launch_fast_t<kEmit, 1, 4, false, SH>(a, nblocks, st);
-    else launch_fast_t<kAbsorb, 1, 4, false, SH>(a, nblocks, st);
+    if (a.unit_mmr) {
+      if (dir == kEmit) launch_fast_t<kEmit, 1, 4, false, SH, true>(a, nblocks, st);
+      else launch_fast_t<kAbsorb, 1, 4, false, SH, true>(a, nblocks, st);
+    } else {
+      if (dir == kEmit) launch_fast_t<kEmit, 1, 4, false, SH>(a, nblocks, st);
+      else launch_fast_t<kAbsorb, 1, 4, false, SH>(a, nblocks, st);
+    }
   } else if (depth >= 2) {
     if (nan_check) launch_fast_pd<2, true, SH>(dir, S, a, nblocks, st);
     else launch_fast_pd<2, false, SH>(dir, S, a, nblocks, st);

@@ -146,6 +146,58 @@ __device__ __forceinline__ double expm1(double x, const Expm1Reg& k) {
   return (x < -37.0) ? -1.0 : y;
 }
 
+// expm1(x) for a Planck exponent x in [0, 600] (every ordinary layer): the sequence of
+// expm1(x, k) above without its range selects (n < 1024, no overflow, x > -37 all hold
+// there), so bit-identical to ocml on that range.  The sweeps route x > 600 (very cold layers
+// at short wavelengths, expm1 >= 2^865) to the full IEEE form.
+__device__ __forceinline__ double expm1_mid(double x, const Expm1Reg& k) {
+  const double n = __builtin_rint(x * c64(0x3ff71547652b82feull));
+  double r = __builtin_fma(c64(0xbfe62e42fefa39efull), n, x);
+  r = __builtin_fma(c64(0xbc7abc9e3b39803full), n, r);
+  double p = __builtin_fma(k.c[0], r, k.c[1]);
+#pragma unroll
+  for (int i = 2; i < 10; ++i) p = __builtin_fma(r, p, k.c[i]);
+  p = r * __builtin_fma(r, p, 0.5);
+  const double s = __builtin_ldexp(1.0, (int)n);
+  const double t = s - 1.0;
+  const double u = __builtin_fma(r, p, r);
+  return __builtin_fma(s, u, t);
+}
+
+// exp(x) for x <= 0 or NaN (a layer transmission exp(-2 sqrt(..) dtau)): ocml's sequence
+// (fm::exp above) with the argument clamped at -1100 instead of its two range selects — below
+// -1075 the final ldexp underflows to the same 0 ocml returns, so bit-identical for every
+// x <= 0; NaN passes through.
+__device__ __forceinline__ double exp_neg(double x) {
+  x = (x < -1100.0) ? -1100.0 : x;
+  const double n = __builtin_rint(x * c64(0x3ff71547652b82feull));
+  double r = __builtin_fma(c64(0xbfe62e42fefa39efull), n, x);
+  r = __builtin_fma(c64(0xbc7abc9e3b39803full), n, r);
+  double p = __builtin_fma(c64(0x3e5ade156a5dcb37ull), r, c64(0x3e928af3fca7ab0cull));
+  p = __builtin_fma(r, p, c64(0x3ec71dee623fde64ull));
+  p = __builtin_fma(r, p, c64(0x3efa01997c89e6b0ull));
+  p = __builtin_fma(r, p, c64(0x3f2a01a014761f6eull));
+  p = __builtin_fma(r, p, c64(0x3f56c16c1852b7b0ull));
+  p = __builtin_fma(r, p, c64(0x3f81111111122322ull));
+  p = __builtin_fma(r, p, c64(0x3fa55555555502a1ull));
+  p = __builtin_fma(r, p, c64(0x3fc5555555555511ull));
+  p = __builtin_fma(r, p, c64(0x3fe000000000000bull));
+  p = __builtin_fma(r, p, 1.0);
+  p = __builtin_fma(r, p, 1.0);
+  return __builtin_ldexp(p, (int)n);
+}
+
+// 1 / b within one ulp: the reciprocal part of the division core below (rcp and two
+// Newton-Raphson steps) without the quotient's final residual correction.  Used where the
+// result only scales a sum (1 / chi of the flux update), so an ulp is not amplified.
+__device__ __forceinline__ double rcp_nr(double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  double e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-b, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+
 // a / b: LLVM's fp64 division core (rcp, two Newton-Raphson steps, quotient, one residual
 // correction) without the div_scale / div_fmas / div_fixup range guards.
 __device__ __forceinline__ double div(double a, double b) {

@@ -536,6 +536,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     f.conv = c->d_conv;
     f.bs = atm_stride(c);
     f.n_atm = c->n_atm;
+    f.unit_mmr = c->eff ? 1 : 0;
     // per-row partials while the one-lane sweep's LDS stays within 48 KiB (3+ blocks per CU)
     f.red_rows = c->red_rows &&
                  (size_t)16 * ns * 4 * sizeof(double) + (size_t)ns * sizeof(FastStepS) <=
