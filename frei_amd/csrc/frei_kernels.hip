@@ -398,8 +398,9 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
   const double E = (w0 > 0.1) ? ((1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0)) : 1.0;
   const double Emw = E - w0;
   const double q = fm::div(fm::div(B1 - B2, dtau), 2.0 * E);
-  coef_tail(w0, dtau, B1, B2, fm::sqrt(E * Emw), fm::sqrt(fm::div(Emw, E)), q,
-            fm::div(kPi * (1.0 - w0), Emw), c);
+  // E = 1 lanes take pi like coef_e1, so both forms give the same bits on them
+  const double pi_w = (w0 > 0.1) ? fm::div(kPi * (1.0 - w0), Emw) : kPi;
+  coef_tail(w0, dtau, B1, B2, fm::sqrt(E * Emw), fm::sqrt(fm::div(Emw, E)), q, pi_w, c);
 }
 
 // Step whose w0 <= 0.1 (E = 1): E * Emw, Emw / E and Bprime / (2 E) are exact without the
