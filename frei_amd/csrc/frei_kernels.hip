@@ -35,6 +35,9 @@ __device__ __forceinline__ double planck(double c1, double lk, double T) {
 #ifndef FREI_EXPM1_VREG
 #define FREI_EXPM1_VREG 1
 #endif
+#ifndef FREI_PI_E1   // E = 1 lanes: pi (1 - w0) / (1 - w0) taken as pi (within an ulp)
+#define FREI_PI_E1 1
+#endif
 // The sweeps' Planck values: expm1 coefficients in VGPRs (fm::Expm1Reg, loaded once), the
 // range-select-free expm1 for exponents <= 600 and an IEEE fallback branch (execz-skipped)
 // for the rare lanes above — cold layers at short wavelengths, where expm1 passes 2^865 and
@@ -399,7 +402,11 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
   const double Emw = E - w0;
   const double q = fm::div(fm::div(B1 - B2, dtau), 2.0 * E);
   // E = 1 lanes take pi like coef_e1, so both forms give the same bits on them
+#if FREI_PI_E1
   const double pi_w = (w0 > 0.1) ? fm::div(kPi * (1.0 - w0), Emw) : kPi;
+#else
+  const double pi_w = fm::div(kPi * (1.0 - w0), Emw);
+#endif
   coef_tail(w0, dtau, B1, B2, fm::sqrt(E * Emw), fm::sqrt(fm::div(Emw, E)), q, pi_w, c);
 }
 
@@ -410,8 +417,14 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
 // the whole wave qualifies.
 __device__ __forceinline__ void coef_e1(double w0, double dtau, double B1, double B2,
                                         StepCoef& c) {
-  const double sq = fm::sqrt(1.0 - w0);
+  const double Emw = 1.0 - w0;
+  const double sq = fm::sqrt(Emw);
+#if FREI_PI_E1
   coef_tail(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5, kPi, c);
+#else
+  coef_tail(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5,
+            fm::div(kPi * (1.0 - w0), Emw), c);
+#endif
 }
 
 struct PreCoef {

@@ -168,20 +168,34 @@ __device__ __forceinline__ double expm1_mid(double x, const Expm1Reg& k) {
 // (fm::exp above) with the argument clamped at -1100 instead of its two range selects — below
 // -1075 the final ldexp underflows to the same 0 ocml returns, so bit-identical for every
 // x <= 0; NaN passes through.
+// exp_neg's Horner terms as VOP3 fma with SGPR coefficients: otherwise the compiler keeps the
+// coefficients in VGPRs and copies each into the accumulator of a two-address v_fmac (one
+// extra move per term) — 174 vs 183 VALU instructions per flux update and -6 % sweep time
+// at 500k despite a few SGPR spills (profiles/r02_ab_exp_sc.txt)
+#ifndef FREI_EXP_SC
+#define FREI_EXP_SC 1
+#endif
+__device__ __forceinline__ double hfma(double r, double p, unsigned long long c) {
+#if FREI_EXP_SC
+  return fma_sc(r, p, c64(c));
+#else
+  return __builtin_fma(r, p, c64(c));
+#endif
+}
 __device__ __forceinline__ double exp_neg(double x) {
   x = (x < -1100.0) ? -1100.0 : x;
   const double n = __builtin_rint(x * c64(0x3ff71547652b82feull));
   double r = __builtin_fma(c64(0xbfe62e42fefa39efull), n, x);
   r = __builtin_fma(c64(0xbc7abc9e3b39803full), n, r);
   double p = __builtin_fma(c64(0x3e5ade156a5dcb37ull), r, c64(0x3e928af3fca7ab0cull));
-  p = __builtin_fma(r, p, c64(0x3ec71dee623fde64ull));
-  p = __builtin_fma(r, p, c64(0x3efa01997c89e6b0ull));
-  p = __builtin_fma(r, p, c64(0x3f2a01a014761f6eull));
-  p = __builtin_fma(r, p, c64(0x3f56c16c1852b7b0ull));
-  p = __builtin_fma(r, p, c64(0x3f81111111122322ull));
-  p = __builtin_fma(r, p, c64(0x3fa55555555502a1ull));
-  p = __builtin_fma(r, p, c64(0x3fc5555555555511ull));
-  p = __builtin_fma(r, p, c64(0x3fe000000000000bull));
+  p = hfma(r, p, 0x3ec71dee623fde64ull);
+  p = hfma(r, p, 0x3efa01997c89e6b0ull);
+  p = hfma(r, p, 0x3f2a01a014761f6eull);
+  p = hfma(r, p, 0x3f56c16c1852b7b0ull);
+  p = hfma(r, p, 0x3f81111111122322ull);
+  p = hfma(r, p, 0x3fa55555555502a1ull);
+  p = hfma(r, p, 0x3fc5555555555511ull);
+  p = hfma(r, p, 0x3fe000000000000bull);
   p = __builtin_fma(r, p, 1.0);
   p = __builtin_fma(r, p, 1.0);
   return __builtin_ldexp(p, (int)n);

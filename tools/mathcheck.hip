@@ -1,5 +1,6 @@
-// Bitwise check of frei_math.h (fm::exp / expm1 / div / sqrt) against the ocml / IEEE forms
-// on the GPU: random inputs over the ranges the sweep uses (and well beyond), plus edge cases.
+// Bitwise check of frei_math.h (fm::exp / expm1 / div / sqrt, exp_neg, expm1_mid) against the
+// ocml / IEEE forms on the GPU, and rcp_nr within one ulp: random inputs over the ranges the
+// sweep uses (and well beyond), plus edge cases.
 //   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -std=c++17 -Ifrei_amd/csrc \
 //         tools/mathcheck.hip -o tools/mathcheck && ./tools/mathcheck
 // Prints mismatch counts per function and range; exit status 1 on any mismatch inside the
@@ -39,9 +40,18 @@ __global__ void check(int kind, double lo, double hi, uint64_t n, unsigned long 
       const double y = lo + (hi - lo) * unif(i, 9);
       const double b = ldexp(1.0 + unif(i, 10), (int)floor(y)) * (unif(i, 11) < 0.5 ? -1 : 1);
       got = fm::div(a, b); ref = a / b; x = a;
-    } else {
+    } else if (kind == 3) {
       x = ldexp(1.0 + unif(i, 12), (int)floor(x));
       got = fm::sqrt(x); ref = ::sqrt(x);
+    } else if (kind == 4) {
+      got = fm::exp_neg(x); ref = ::exp(x);
+    } else if (kind == 5) {
+      got = fm::expm1_mid(x, fm::expm1_regs()); ref = ::expm1(x);
+    } else {   // rcp_nr: within one ulp of the correctly rounded 1 / b
+      const double b = ldexp(1.0 + unif(i, 13), (int)floor(x)) * (unif(i, 14) < 0.5 ? -1 : 1);
+      got = fm::rcp_nr(b); ref = 1.0 / b; x = b;
+      const long long d = __double_as_longlong(got) - __double_as_longlong(ref);
+      if (d >= -1 && d <= 1) got = ref;
     }
     if (!same(got, ref)) {
       if (atomicAdd(bad, 1ull) == 0) { example[0] = x; example[1] = got; example[2] = ref; }
@@ -60,6 +70,9 @@ __global__ void edges(unsigned long long* bad) {
     b += !same(fm::expm1(x), ::expm1(x));
     if (x >= 0x1p-767 || x == 0.0 || x == inf || isnan(x)) b += !same(fm::sqrt(x), ::sqrt(x));
   }
+  const double xn[] = {0.0, -0.0, -1e-300, -1.0, -745.1, -1074.9, -1075.0, -1075.1, -1100.0,
+                       -1100.5, -1e6, -inf, nan};
+  for (double x : xn) b += !same(fm::exp_neg(x), ::exp(x));
   b += !same(fm::div_big(3.0, inf), 0.0);
   b += !same(fm::div_big(3.0, 0x1p1000), 3.0 / 0x1p1000);
   *bad = b;
@@ -80,6 +93,9 @@ int main() {
       {"div   2^[-1070, 1020] (guards dropped: may differ)", 2, -1070.0, 1020.0, false},
       {"sqrt  2^[-767, 1023]", 3, -767.0, 1023.0, true},
       {"sqrt  2^[-1074, -767] (scaling dropped: may differ)", 3, -1074.0, -767.0, false},
+      {"exp_neg [-1200, 0] vs exp (sweep transmission)", 4, -1200.0, 0.0, true},
+      {"expm1_mid [0, 600] vs expm1 (Planck, ordinary layers)", 5, 0.0, 600.0, true},
+      {"rcp_nr within 1 ulp, |b| in 2^[-450, 450]", 6, -450.0, 450.0, true},
   };
   const uint64_t n = 1ull << 28;
   int fail = 0;
