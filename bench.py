@@ -49,6 +49,9 @@ def parse():
                     help="N > 1 exchange: the engine's P2P mailboxes over xGMI (default; falls "
                          "back to RCCL if they cannot be set up), RCCL all-gather, or the host "
                          "hook (lets several ranks share one GPU to rehearse the multi-rank flow)")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="with --gpus 1: still join the exchange (a one-rank P2P mailbox or "
+                         "RCCL communicator), to time its per-sweep cost on one GPU")
     ap.add_argument("--no-per-species", action="store_true",
                     help="skip the per-species (no K3 contraction) measurement")
     ap.add_argument("--per-species-steps", type=int, default=6)
@@ -238,13 +241,18 @@ def _emit_result(line):
     os.write(_RESULT_FD, (json.dumps(line) + "\n").encode())
 
 
-def build_engine(w, tabs, lo, hi, d, kind):
-    """Engine for this rank's slice, joined to the other ranks over ``kind`` (p2p, rccl, host)."""
+def build_engine(w, tabs, lo, hi, d, kind, force=False):
+    """Engine for this rank's slice, joined to the other ranks over ``kind`` (p2p, rccl, host);
+    ``force`` joins a one-rank exchange on a single GPU (cost measurement)."""
     from frei_amd.distributed import host_comm, p2p_comm, rccl_comm
     from frei_amd.engine import Engine
+    from frei_amd.rendezvous import Rendezvous
     comm = None
-    if d.world > 1:
-        comm = {"p2p": p2p_comm, "rccl": rccl_comm, "host": host_comm}[kind](d.rdzv)
+    if d.world > 1 or force:
+        rdzv = d.rdzv if d.rdzv is not None else Rendezvous(1, 0)
+        if force and kind == "rccl":
+            os.environ["FREI_FORCE_RCCL"] = "1"
+        comm = {"p2p": p2p_comm, "rccl": rccl_comm, "host": host_comm}[kind](rdzv)
     return Engine(w["lam"], w["p"], tabs, mmr=w["mmr"], device=d.local, lam_slice=(lo, hi),
                   comm=comm)
 
@@ -284,9 +292,9 @@ def main():
     from frei_amd.opacity import SeparableTable
     from frei_amd.workloads import bytes_per_update, c3
 
-    if a.comm == "host":   # rehearsal: ranks may share the GPUs there are
-        n_dev = max(1, N.device_count())
-        if d.world > n_dev and d.local >= n_dev:
+    n_dev = max(1, N.device_count())
+    if d.world > n_dev:   # rehearsal on fewer GPUs than ranks: ranks share the GPUs there are
+        if d.local >= n_dev:
             # ranks sharing a device need distinct device address layouts
             import ctypes
             hip = ctypes.CDLL("libamdhip64.so")
@@ -303,7 +311,7 @@ def main():
     t_e = time.perf_counter()
     eng, err = None, None
     try:
-        eng = build_engine(w, tabs, lo, hi, d, kind)
+        eng = build_engine(w, tabs, lo, hi, d, kind, a.force_comm)
     except RuntimeError as e:   # e.g. no IPC / peer mapping: fall back to RCCL everywhere
         err = str(e)
     if not d.all_ok(eng is not None):
@@ -313,7 +321,7 @@ def main():
             eng.close()
         comm_note = f"p2p setup failed ({err or 'on a peer rank'}); fell back to RCCL"
         kind = "rccl"
-        eng = build_engine(w, tabs, lo, hi, d, kind)
+        eng = build_engine(w, tabs, lo, hi, d, kind, a.force_comm)
     tables_s = time.perf_counter() - t_e
     # one-time setup: metadata build + species contraction (K3), outside the timed steps
     t_s = time.perf_counter()
@@ -327,7 +335,7 @@ def main():
     # ---- sweep-kernel duration: HIP events on the engine's stream around every sweep launch
     avg_sweep_ms, n_sweeps, xch_ms, n_xch = sweep_kernel_time(eng, max(2, a.steps // 2))
     exchange = None
-    if d.world > 1:   # per-sweep rank exchange, max over ranks
+    if d.world > 1 or a.force_comm:   # per-sweep rank exchange, max over ranks
         what = {"p2p": "P2P mailbox push over xGMI (update-kernel wait)",
                 "rccl": "RCCL all-gather", "host": "host all-gather"}[kind]
         exchange = {"kind": f"{what} of {4 * (nL - 1) * 8} B per rank",
@@ -383,6 +391,21 @@ def main():
             "byte_model": f"8 stale opposite-stream read + 8 live flux write + 16*S = {bpu_ps} B "
                           f"(SURVEY 8(d)'s 24 + 16*S = {24 + 16 * S} B less the dead store the "
                           "T-P loop skips)"}
+        tp = os.path.join(ROOT, "profiles", "traffic_sweep_per_species.json")
+        vp = os.path.join(ROOT, "profiles", "valu_sweep_per_species.json")
+        if os.path.exists(tp):
+            t = json.load(open(tp))
+            if t["workload"] == {"n_lam": n_lam // d.world, "n_layers": nL, "species": S,
+                                 "contracted": False}:
+                per_species["roofline"].update(
+                    traffic=t["hbm_B_per_launch"],
+                    traffic_over_algorithmic=t["traffic_over_algorithmic"],
+                    traffic_source="profiles/traffic_sweep_per_species.json")
+                if os.path.exists(vp):
+                    v = json.load(open(vp))
+                    per_species["roofline"].update(
+                        valu_busy=v["valu_busy"], valu_insts_per_64_updates=v["valu_insts_per_update"],
+                        valu_source="profiles/valu_sweep_per_species.json")
         eng.set_option("precontract", -1)
         eng.path()
     cpu = None
@@ -431,7 +454,8 @@ def main():
                                    "1 step = 1 T-P iteration (emit+absorb)",
                        "n_layers": nL, "n_lambda": n_lam, "n_species": S, "n_T": a.n_T,
                        "parallelism": f"lambda-shard x{d.world}"
-                                      + ("" if d.world == 1 else f" ({kind} exchange per sweep)")},
+                                      + ("" if d.world == 1 and not a.force_comm
+                                         else f" ({kind} exchange per sweep)")},
             "tp_iters_per_s": 1e3 / ms_per_step,
             "exchange": exchange,
             "sweep_path": dict(path, setup_ms=setup_ms, setup_phases_ms=setup_phases,
