@@ -27,6 +27,12 @@ constexpr int kMaxLayers = 1024;
 __host__ __device__ inline int step_layer(int dir, int k, int nL) {
   return dir == kEmit ? k + 1 : nL - 2 - k;
 }
+// The step of direction `dir` whose layer is i (inverse of step_layer), -1 if layer i has none
+// (emit: layer 0; absorb: the top layer).
+__host__ __device__ inline int layer_step(int dir, int i, int nL) {
+  const int k = dir == kEmit ? i - 1 : nL - 2 - i;
+  return (k >= 0 && k < nL - 1) ? k : -1;
+}
 
 // Per sweep step, wave-uniform.
 struct StepP {
@@ -327,6 +333,13 @@ struct UpdateArgs {
   int32_t *flips, *prev_sign, *ndiff;
   int* iter;
   int* conv;
+  // fused reduce + update (launch_update_fused): the sweep's per-block partials, the P2P push
+  // of this rank's sums, the output temperature buffer (T_in is su.T) and the arrival counter
+  const double* part;      // [n_steps*4][nblocks]
+  int nblocks;
+  P2PPush push;
+  double* T_out;
+  unsigned* done;
 };
 
 // LDS bytes of the update kernel (K4/K5): T, dT, p, T before/after absorb, ln p ratios,
@@ -356,6 +369,12 @@ void launch_p2p_handshake(const P2PPush& push, const P2PWait& wait, hipStream_t 
 void launch_setup(const SetupArgs& u, int dir, hipStream_t st, int n_atm = 1);
 void launch_log_ratio(const double* p, double p_top2, int nL, double* lnp, hipStream_t st);
 void launch_update(const UpdateArgs& a, hipStream_t st, int n_atm = 1);
+// Reduce + update in one launch for one atmosphere, local or P2P exchange: one workgroup per
+// layer sums the partials of the (at most two) steps its layer pair needs, pushes its own
+// step's sums to the peers, takes theirs, and writes its layer's T (into a.T_out), history
+// and next-sweep step record; the last workgroup to arrive (a.done) settles the convergence
+// flag.  Bitwise identical to launch_reduce + launch_update.
+void launch_update_fused(const UpdateArgs& a, hipStream_t st);
 void launch_propagate(int64_t n, const double* c1, const double* lk, const double* F1u,
                       const double* F2d, double T1, double T2, const double* dtau,
                       const double* w0, const double* g0, double* F2u, double* F1d,

@@ -1099,20 +1099,26 @@ void launch_log_ratio(const double* p, double p_top2, int nL, double* lnp, hipSt
 }
 
 // ---------------------------------------------------------------- setup (T -> terms)
+// Step records [kb, ke) of the sweep in direction `dir` from temperatures T (only the layers
+// of those steps and the ones above them are read), written by the threads tid = 0, 1, ...
+// of the caller's group (nthr of them).  pmeta / mmr of species s at layer i are read at
+// s * mstride + (i - mbase): [S][n_layers] arrays (mstride n_layers, mbase 0) or one layer's
+// values staged per species (mstride 1, mbase = that layer).
 __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P,
                             const double* tnodes, const SpecMeta* spec, const PMeta* pmeta,
-                            const double* mmr, int dir) {
-  const int nL = u.n_layers;
-  const int ns = nL - 1;
+                            const double* mmr, int dir, int kb, int ke, int tid, int nthr,
+                            int mstride, int mbase) {
   const int nS = u.n_species;
+  const int nL = u.n_layers;
+  auto MI = [&](int s, int i) { return (int64_t)s * mstride + (i - mbase); };
   // mixing ratio of species s at layer i: the chemistry table at the layer's current T
   // (kappa's chemistry(T, p) call, opacity.py:246-248), else the fixed per-layer arrays
   auto MMR = [&](int s, int i) {
     return u.chem.tab ? chem_mmr_at(u.chem, s, u.chem.pj[i], u.chem.pz[i], T[i])
-                      : mmr[(int64_t)s * nL + i];
+                      : mmr[MI(s, i)];
   };
   if (u.fast && u.shared) {
-    for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+    for (int k = kb + tid; k < ke; k += nthr) {
       const int i = step_layer(dir, k, nL);
       FastStepS* f = u.ssteps + k;
       const int top = (dir == kEmit && i == nL - 1) ? 1 : 0;
@@ -1124,7 +1130,7 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
       f->dm = (P[i] - p2) / u.g;
       int64_t off;
       double wlo, whi;
-      fast_term(spec[0], pmeta[i], tnodes, T[i], off, wlo, whi);
+      fast_term(spec[0], pmeta[MI(0, i)], tnodes, T[i], off, wlo, whi);
       f->off = off;
       f->wlo = wlo;
       f->whi = whi;
@@ -1133,7 +1139,7 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
     return;
   }
   if (u.fast) {
-    for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+    for (int k = kb + tid; k < ke; k += nthr) {
       const int i = step_layer(dir, k, nL);
       FastStep* f = u.fsteps + k;
       const int top = (dir == kEmit && i == nL - 1) ? 1 : 0;
@@ -1144,8 +1150,8 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
       const double p2 = top ? u.p_top2 : P[i + 1];
       f->dm = (P[i] - p2) / u.g;
     }
-    for (int idx = threadIdx.x; idx < ns * kMaxFastS; idx += blockDim.x) {
-      const int k = idx / kMaxFastS, s = idx % kMaxFastS;
+    for (int idx = tid; idx < (ke - kb) * kMaxFastS; idx += nthr) {
+      const int k = kb + idx / kMaxFastS, s = idx % kMaxFastS;
       FastStep* f = u.fsteps + k;
       if (s >= nS) {
         f->off[s] = 0;
@@ -1155,7 +1161,7 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
       const int i = step_layer(dir, k, nL);
       int64_t off;
       double wlo, whi;
-      fast_term(spec[s], pmeta[(int64_t)s * nL + i], tnodes, T[i], off, wlo, whi);
+      fast_term(spec[s], pmeta[MI(s, i)], tnodes, T[i], off, wlo, whi);
       f->off[s] = off;
       f->wlo[s] = wlo;
       f->whi[s] = whi;
@@ -1163,7 +1169,7 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
     }
     return;
   }
-  for (int k = threadIdx.x; k < ns; k += blockDim.x) {   // generic kernel's step records
+  for (int k = kb + tid; k < ke; k += nthr) {   // generic kernel's step records
     const int i = step_layer(dir, k, nL);
     StepP sp;
     sp.layer = i;
@@ -1175,10 +1181,10 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
     sp.pad = 0;
     u.steps[k] = sp;
   }
-  for (int idx = threadIdx.x; idx < ns * nS; idx += blockDim.x) {
-    const int k = idx / nS, s = idx % nS;
+  for (int idx = tid; idx < (ke - kb) * nS; idx += nthr) {
+    const int k = kb + idx / nS, s = idx % nS;
     const int i = step_layer(dir, k, nL);
-    u.terms[idx] = make_term(spec[s], pmeta[(int64_t)s * nL + i], tnodes, u.tperm, MMR(s, i),
+    u.terms[(int64_t)k * nS + s] = make_term(spec[s], pmeta[MI(s, i)], tnodes, u.tperm, MMR(s, i),
                              T[i], u.fast);
   }
 }
@@ -1210,7 +1216,8 @@ __device__ inline void atm_view(UpdateArgs& a, int m) {
 
 __global__ void setup_kernel(SetupArgs u, int dir) {
   atm_view(u, blockIdx.x);
-  setup_sweep(u, u.T, u.p, u.tnodes, u.spec, u.pmeta, u.mmr, dir);
+  setup_sweep(u, u.T, u.p, u.tnodes, u.spec, u.pmeta, u.mmr, dir, 0, u.n_layers - 1,
+              threadIdx.x, blockDim.x, u.n_layers, 0);
 }
 
 // ---------------------------------------------------------------- K4/K5: update
@@ -1380,7 +1387,193 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
 #ifndef FREI_UPD_NOSETUP  // diagnostic ablation build
   if (a.next_dir >= 0)
     setup_sweep(a.su, sT, sP, sTn, meta ? sSp : a.su.spec, meta ? sPm : a.su.pmeta,
-                meta ? sMm : a.su.mmr, a.next_dir);
+                meta ? sMm : a.su.mmr, a.next_dir, 0, ns, threadIdx.x, blockDim.x, nL, 0);
+#endif
+}
+
+// ---------------------------------------------------------------- reduce + update, fused
+// One workgroup per layer l: the per-block partial sums of the steps whose
+// layers are l and l + 1 (the two dT values the next sweep's step record of layer l needs),
+// summed in reduce_kernel's order; with P2P, wave 1 pushes the workgroup's own step's sums
+// while wave 0 takes the peers' (rank order, own rank from registers); dT (layer_dT) in wave
+// 0; then thread 0 does layer l's bookkeeping as in update_kernel and writes its new T into
+// T_out (the other temperature buffer: neighbouring workgroups still read T_in) while wave 1
+// writes the next sweep's record of layer l.  Every input is loaded at the start.  The
+// convergence AND over layers rides on one arrival counter: each workgroup adds
+// 1 + 65536 * (layer not converged); the last to arrive sets iter / conv and rearms it.
+__global__ __launch_bounds__(256) void update_fused_kernel(UpdateArgs a) {
+#ifdef FREI_UPD_EMPTY  // diagnostic ablation build: launch floor
+  return;
+#endif
+  const int l = blockIdx.x;
+  const int nL = a.su.n_layers;
+  const int dir = a.dir;
+  const int tid = threadIdx.x;
+  const double* Tin = a.su.T;
+  extern __shared__ __attribute__((aligned(16))) double sh[];
+  double* sTn = sh;                 // [nL] new T of layers l, l + 1 (the setup's T view)
+  double* sP = sTn + nL;            // [nL] p of layers l, l + 1 (the setup's p view)
+  double* sNodes = sP + nL;         // [n_tnodes] sorted T nodes
+  __shared__ double wsum[4][8];
+  __shared__ double tot[8];         // this rank's sums of steps k0 (0..3) and k1 (4..7)
+  __shared__ PMeta sPm[kMaxFastS];  // layer l's metadata per species (setup)
+  __shared__ SpecMeta sSp[kMaxFastS];
+  __shared__ double sMm[kMaxFastS];
+  const int k0 = layer_step(dir, l, nL);
+  const int k1 = l + 1 < nL ? layer_step(dir, l + 1, nL) : -1;
+  const int kn = a.next_dir >= 0 ? layer_step(a.next_dir, l, nL) : -1;
+  const int S = a.su.n_species;
+  const bool stage = S <= kMaxFastS;
+  // ---- every input up front: unconditional loads at clamped indices (no branch between a
+  // load and the next one), consumed after the partial sums have landed
+  const int conv = *a.conv;
+  const int it = *a.iter;
+  const int ntn = a.su.n_tnodes;
+  const double rNode = a.su.tnodes[tid < ntn ? tid : ntn - 1];
+  const int li = min(l + (tid & 1), nL - 1);
+  const int li1 = min(li + 1, nL - 1);
+  const int kd = (tid & 1) ? k1 : k0;
+  const bool top = (dir == kEmit && li == nL - 1);
+  const double T1 = Tin[li];
+  const double rT2 = Tin[li1];
+  const double p1 = a.su.p[li];
+  const double rp2 = a.su.p[li1];
+  const double lnp = a.lnp[li];
+  const double Tb = a.Tb[l], Ta = a.Ta[l];
+  int flips = a.flips[l], prev = a.prev_sign[l], nd = a.ndiff[l];
+  const int sm = min(max(tid - 64, 0), S - 1);
+  const PMeta rPm = a.su.pmeta[(int64_t)sm * nL + l];
+  const SpecMeta rSp = a.su.spec[sm];
+  const double rMm = a.su.mmr[(int64_t)sm * nL + l];
+  const double T2 = top ? T1 : rT2;
+  const double p2 = top ? a.su.p_top2 : rp2;
+  const double Tl = T1;              // lanes with (tid & 1) == 0: layer l
+  if (!a.force && conv) {    // converged: carry T into the output buffer
+    if (tid == 0) a.T_out[l] = Tl;
+    return;
+  }
+  // ---- this rank's sums, reduce_kernel's order (strided per thread, wave butterfly, waves)
+#ifdef FREI_UPD_NOSUM  // diagnostic ablation build
+  if (false) {
+#else
+  if (k0 >= 0 || k1 >= 0) {
+#endif
+    const double* pj[8];
+    for (int j = 0; j < 8; ++j) {
+      const int k = (j < 4) ? (k0 >= 0 ? k0 : k1) : (k1 >= 0 ? k1 : k0);
+      pj[j] = a.part + (int64_t)(k * 4 + (j & 3)) * a.nblocks;
+    }
+    double acc[8];
+    for (int j = 0; j < 8; ++j) acc[j] = 0.0;
+#pragma unroll 2
+    for (int b = tid; b < a.nblocks; b += 256)
+      for (int j = 0; j < 8; ++j) acc[j] += pj[j][b];
+    for (int j = 0; j < 8; ++j)
+      for (int o = 32; o > 0; o >>= 1) acc[j] += __shfl_xor(acc[j], o, 64);
+    if ((tid & 63) == 0)
+      for (int j = 0; j < 8; ++j) wsum[tid >> 6][j] = acc[j];
+  }
+  // stage the setup's inputs in LDS (their loads were issued at the start)
+  if (tid < ntn) sNodes[tid] = rNode;
+  for (int q = tid + 256; q < ntn; q += 256) sNodes[q] = a.su.tnodes[q];
+  if (kn >= 0) {
+    const int s = tid - 64;
+    if (stage && s >= 0 && s < S) {
+      sPm[s] = rPm;
+      sSp[s] = rSp;
+      sMm[s] = rMm;
+    }
+    if (tid < 2 && l + tid < nL) sP[l + tid] = p1;   // lane 1: layer l + 1
+    if (tid == 1 && l + 1 < nL) sTn[l + 1] = T1;      // layer l + 1 before its update
+  }
+  __syncthreads();
+  if (tid < 8) tot[tid] = ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
+  __syncthreads();
+  const long long t0 = wall_clock64();
+  if (a.p2p.mbox && tid == 64 && k0 >= 0) p2p_push_values(a.push, (int64_t)k0 * 4, tot, 4);
+  if (tid < 64) {
+    // all ranks' sums in rank order (lanes 0..7), then dT of layers l, l + 1 (lanes 0, 1)
+    double v = 0.0;
+    const int k = tid < 4 ? k0 : k1;
+    if (tid < 8 && k >= 0) {
+      v = tot[tid];
+      if (a.p2p.mbox) {
+        const double own = v;
+        for (int r = 0; r < a.p2p.nranks; ++r) {
+          const double x =
+              (r == a.push.rank) ? own : p2p_take(a.p2p, r, (int64_t)k * 4 + (tid & 3), t0);
+          v = (r == 0) ? x : v + x;
+        }
+      }
+    }
+    const int base = (tid & 1) * 4;
+    double F[4];
+    for (int q = 0; q < 4; ++q) F[q] = __shfl(v, base + q, 64);
+    if (tid < 4 && k0 >= 0 && a.bol_out) a.bol_out[(int64_t)l * 4 + tid] = v;
+    if (tid == 0 && l == 0 && a.p2p.mbox && a.p2p.wait_ticks)
+      atomicAdd(a.p2p.wait_ticks, (unsigned long long)(wall_clock64() - t0));
+    double d = 0.0;
+    if (tid < 2 && kd >= 0) {
+#ifdef FREI_UPD_NODT  // diagnostic ablation build
+      d = 1e-3 * (F[0] - F[1]) + T2 * 1e-9 + p2 * 1e-20 + lnp * 0;
+#else
+      d = layer_dT(F, T1, T2, p1, p2, lnp, a.su.g, a.m_bar, a.alpha);
+#endif
+      sTn[li] = T1 - d;
+    }
+    if (tid == 0) {
+      // layer l's bookkeeping (update_kernel's expressions)
+      const double dT = d;
+      const double Tnew = Tl - dT;
+      if (a.dT_out) a.dT_out[l] = dT;
+      bool c = true;
+      if (a.track) {
+        if (dir == kEmit) {
+          a.Tb[l] = Tnew;
+        } else {
+          if (it < a.hist_cap) {
+            a.hist[((int64_t)it * 2 + 0) * nL + l] = Tb;
+            a.hist[((int64_t)it * 2 + 1) * nL + l] = Tnew;
+          }
+          const double d0 = Tb - Ta, d1 = Tnew - Tb;
+          for (int q = (it > 0 ? 0 : 1); q < 2; ++q) {
+            const double dd = q == 0 ? d0 : d1;
+            const int sgn = (dd > 0) - (dd < 0);
+            if (nd > 0 && sgn != prev) ++flips;
+            prev = sgn;
+            ++nd;
+          }
+          a.flips[l] = flips;
+          a.prev_sign[l] = prev;
+          a.ndiff[l] = nd;
+          a.Ta[l] = Tnew;
+          c = (flips > a.n_zero_crossings) || (fabs(dT) < a.convergence_dT);
+        }
+      }
+      a.T_out[l] = Tnew;
+      if (kd < 0) sTn[l] = Tnew;
+      if (a.track && dir == kAbsorb) {
+        const unsigned old = __hip_atomic_fetch_add(a.done, 1u + (c ? 0u : 65536u),
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((old & 0xffffu) == gridDim.x - 1) {   // last layer in: every other one has counted
+          const unsigned nc = (old >> 16) + (c ? 0u : 1u);
+          *a.iter = it + 1;
+          if (nc == 0 && a.stop_on_conv) *a.conv = 1;
+          __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
+  __syncthreads();   // sTn of layers l, l + 1
+#ifndef FREI_UPD_NOSETUP  // diagnostic ablation build
+  if (kn >= 0 && tid >= 64) {
+    if (stage)
+      setup_sweep(a.su, sTn, sP, sNodes, sSp, sPm, sMm, a.next_dir, kn, kn + 1, tid - 64,
+                  blockDim.x - 64, 1, l);
+    else
+      setup_sweep(a.su, sTn, sP, sNodes, a.su.spec, a.su.pmeta, a.su.mmr, a.next_dir, kn,
+                  kn + 1, tid - 64, blockDim.x - 64, nL, 0);
+  }
 #endif
 }
 
@@ -1753,6 +1946,11 @@ void launch_update(const UpdateArgs& a, hipStream_t st, int n_atm) {
   const size_t shm = update_lds_bytes(a.su.n_layers, a.su.n_tnodes, a.su.n_species,
                                       a.meta_in_lds != 0);
   hipLaunchKernelGGL(update_kernel, dim3(n_atm), dim3(256), shm, st, a);
+}
+
+void launch_update_fused(const UpdateArgs& a, hipStream_t st) {
+  const size_t shm = (2 * (size_t)a.su.n_layers + a.su.n_tnodes) * sizeof(double);
+  hipLaunchKernelGGL(update_fused_kernel, dim3(a.su.n_layers), dim3(256), shm, st, a);
 }
 
 void launch_propagate(int64_t n, const double* c1, const double* lk, const double* F1u,

@@ -108,6 +108,11 @@ struct frei_ctx {
   // state
   double *d_Fu = nullptr, *d_Fd = nullptr, *d_T = nullptr, *d_dT = nullptr,
          *d_dtaus = nullptr, *d_bol = nullptr;
+  // the fused reduce + update writes the new temperatures into the other buffer and the two
+  // swap (d_T is always the current one); d_done: its arrival counter
+  double* d_T_alt = nullptr;
+  unsigned* d_done = nullptr;
+  int fused_update = 1;                 // FREI_FUSED_UPDATE=0: separate reduce and update kernels
   // tables
   std::vector<Species> sp;
   std::vector<double> mmr;
@@ -585,7 +590,12 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     wait.err = c->d_comm_err;
     wait.wait_ticks = c->timing ? c->d_wait_ticks : nullptr;
   }
-  {
+  // one launch for reduce + update: one atmosphere, exchange local or P2P (RCCL and the host
+  // hook need the rank's sums in memory between the two kernels)
+  const bool fused = c->fused_update && c->n_atm == 1 && !c->comm &&
+                     !(c->nranks > 1 && c->host_ag) &&
+                     (2 * (size_t)c->nL + c->tnodes.size()) * sizeof(double) <= 32 * 1024;
+  if (!fused) {
     const AtmStride bs = atm_stride(c);
     launch_reduce(c->d_part, nb_run, c->d_Fb, ns * 4, c->d_conv, o.force, c->stream,
                   c->n_atm, bs.part, bs.fb, c->d_mbox ? &push : nullptr);
@@ -650,6 +660,17 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   const int S_meta = c->eff ? 1 : c->S;
   u.meta_in_lds = update_lds_bytes(c->nL, (int)c->tnodes.size(), S_meta, true) <=
                   std::min<size_t>(c->lds_per_block, 64 * 1024);
+  if (fused) {
+    u.part = c->d_part;
+    u.nblocks = nb_run;
+    u.push = push;
+    u.T_out = c->d_T_alt;
+    u.done = c->d_done;
+    launch_update_fused(u, c->stream);
+    HIP_TRY(hipGetLastError());
+    std::swap(c->d_T, c->d_T_alt);
+    return 0;
+  }
   launch_update(u, c->stream, c->n_atm);
   HIP_TRY(hipGetLastError());
   return 0;
@@ -704,7 +725,7 @@ bool ready(frei_ctx* c) { return c && c->grid_set; }
 const char* const kOptionNames[] = {"prefetch_depth", "shared", "shared_max_blocks",
                                     "precontract", "depth4_max_blocks", "pair_max_blocks",
                                     "quad_max_blocks", "red_rows", "red_stage", "group_q",
-                                    nullptr};
+                                    "fused_update", nullptr};
 int set_option(frei_ctx* c, const std::string& k, int v) {
   if (k == "prefetch_depth") c->prefetch_depth = v;
   else if (k == "shared") c->shared_mode = v < 0 ? -1 : (v ? 1 : 0);
@@ -716,6 +737,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "red_rows") c->red_rows = v != 0;
   else if (k == "red_stage") c->red_stage = v != 0;
   else if (k == "group_q") c->group_q = (v == 1 || v == 2 || v == 4) ? v : 0;
+  else if (k == "fused_update") c->fused_update = v != 0;
   else return fail("unknown option '" + k + "'");
   c->meta_dirty = true;
   return 0;
@@ -789,7 +811,8 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
       (rc = dalloc(&c->d_sig, n_lam)) || (rc = dalloc(&c->d_ftoa, n_lam)) ||
       (rc = dalloc(&c->d_wtr, n_lam)) || (rc = dalloc(&c->d_p, NL)) || (rc = dalloc(&c->d_lnp, NL)) ||
       (rc = dalloc(&c->d_Fu, F)) || (rc = dalloc(&c->d_Fd, F)) ||
-      (rc = dalloc(&c->d_T, NL * A)) || (rc = dalloc(&c->d_dT, NL * A)) ||
+      (rc = dalloc(&c->d_T, NL * A)) || (rc = dalloc(&c->d_T_alt, NL * A)) ||
+      (rc = dalloc(&c->d_done, 1)) || (rc = dalloc(&c->d_dT, NL * A)) ||
       (rc = dalloc(&c->d_bol, NL * 4 * A)) || (rc = dalloc(&c->d_mmr, NS * NL * A)) ||
       (rc = dalloc(&c->d_steps, ns * A)) || (rc = dalloc(&c->d_terms, ns * NS * A)) ||
       (rc = dalloc(&c->d_fsteps, ns * A)) || (rc = dalloc(&c->d_ssteps, ns * A)) ||
@@ -807,7 +830,8 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
       return bail(fail("hipEventCreate failed"));
   if (hipMemset(c->d_Fu, 0, F * sizeof(double)) != hipSuccess ||
       hipMemset(c->d_Fd, 0, F * sizeof(double)) != hipSuccess ||
-      hipMemset(c->d_conv, 0, sizeof(int) * A) != hipSuccess)
+      hipMemset(c->d_conv, 0, sizeof(int) * A) != hipSuccess ||
+      hipMemset(c->d_done, 0, sizeof(unsigned)) != hipSuccess)
     return bail(fail("hipMemset failed"));
   if (A > 1 && hipHostMalloc((void**)&c->h_conv, 2 * A * sizeof(int)) != hipSuccess)
     return bail(fail("hipHostMalloc failed"));
@@ -848,12 +872,13 @@ int frei_ctx_destroy(frei_ctx* c) {
   dfree(c->d_ones);
   dfree(c->d_prow);
   double* dd[] = {c->d_c1, c->d_lk, c->d_sig, c->d_ftoa, c->d_wtr, c->d_p, c->d_lnp,
-                  c->d_Fu, c->d_Fd, c->d_T, c->d_dT, c->d_dtaus, c->d_bol, c->d_tnodes, c->d_mmr, c->d_part,
+                  c->d_Fu, c->d_Fd, c->d_T, c->d_T_alt, c->d_dT, c->d_dtaus, c->d_bol, c->d_tnodes, c->d_mmr, c->d_part,
                   c->d_Fb, c->d_Fb_all, c->d_Tb, c->d_Ta, c->d_hist};
   for (double* p : dd)
     if (p) (void)hipFree(p);
   void* vv[] = {c->d_smeta, c->d_pmeta, c->d_tperm, c->d_steps, c->d_terms, c->d_fsteps,
-                c->d_ssteps, c->d_conv, c->d_iter, c->d_flips, c->d_prev, c->d_ndiff};
+                c->d_ssteps, c->d_conv, c->d_iter, c->d_flips, c->d_prev, c->d_ndiff,
+                c->d_done};
   for (void* p : vv)
     if (p) (void)hipFree(p);
   if (c->h_flag) (void)hipHostFree(c->h_flag);

@@ -222,7 +222,9 @@ int frei_ctx_path(frei_ctx* ctx, int* flags);
  * (K3 species contraction: 1 on when it applies / 0 off / -1 automatic), "group_q" (lanes per
  * wavelength 1, 2, 4 or 0 = automatic), "shared" (LDS step table 1/0/-1), "prefetch_depth",
  * "shared_max_blocks", "pair_max_blocks", "quad_max_blocks", "depth4_max_blocks",
- * "red_rows", "red_stage".  Takes effect at the next metadata build. */
+ * "red_rows", "red_stage" (take effect at the next metadata build), "fused_update" (1: one
+ * launch for the partial-sum reduction and the T update when the exchange is local or P2P;
+ * 0: two kernels; bitwise identical results; takes effect at the next sweep). */
 int frei_set_option(frei_ctx* ctx, const char* name, int value);
 /* Host wall-clock milliseconds of the last metadata build (the one-time setup before the
  * first sweep after tables/mmr change), by phase: [0] per-(species, layer) brackets on the

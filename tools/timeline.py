@@ -2,7 +2,7 @@
 
     python tools/timeline.py path/to/run_kernel_trace.csv
 
-For every sweep -> reduce -> (all-gather) -> update cycle it attributes the kernel durations
+For every sweep -> reduce -> (all-gather) -> update cycle (or sweep -> fused update) it attributes the kernel durations
 and the idle gaps between consecutive kernels (end of one to start of the next), then
 prints the medians: what a T-P half-iteration costs beyond the sweep itself.
 """
@@ -12,9 +12,11 @@ import sys
 
 
 def kind(name):
-    for k in ("sweep", "reduce_kernel", "update_kernel", "ncclDevKernel", "AllGather"):
+    for k in ("sweep", "reduce_kernel", "update_kernel", "update_fused", "ncclDevKernel",
+              "AllGather"):
         if k in name:
             return {"reduce_kernel": "reduce", "update_kernel": "update",
+                    "update_fused": "update",
                     "ncclDevKernel": "allgather", "AllGather": "allgather"}.get(k, k)
     return None
 
