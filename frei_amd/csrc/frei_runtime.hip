@@ -5,6 +5,7 @@
 // (one ncclAllGather of n_layers*4 doubles per sweep).
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cctype>
 #include <chrono>
 #include <cmath>
@@ -111,8 +112,21 @@ struct frei_ctx {
   // the fused reduce + update writes the new temperatures into the other buffer and the two
   // swap (d_T is always the current one); d_done: its arrival counter
   double* d_T_alt = nullptr;
+  double* d_T_home = nullptr;           // the buffer d_T names after a host upload
   unsigned* d_done = nullptr;
   int fused_update = 1;                 // FREI_FUSED_UPDATE=0: separate reduce and update kernels
+  // T-P iterations replayed from a captured hipGraph (frei_iterate / frei_run, timing off,
+  // single rank): g_key holds the hashes of one iteration's kernel arguments; any change
+  // (pointers, options, loop parameters) re-captures.  Off by default (FREI_GRAPH=1 turns it
+  // on): measured no faster than stream launches, whose dispatch already overlaps the
+  // previous kernel (profiles/r02_ab_graph.txt).
+  int use_graph = 0;
+  int graph_iters = 4;                  // iterations per captured graph
+  hipGraphExec_t g_exec = nullptr;
+  std::vector<uint64_t> g_key;
+  int g_captures = 0, g_replays = 0;     // frei_graph_info
+  std::vector<uint64_t>* keys = nullptr;  // collecting run_sweep's argument hashes
+  bool dry = false;                       // run_sweep computes hashes only (no launches)
   // tables
   std::vector<Species> sp;
   std::vector<double> mmr;
@@ -488,7 +502,17 @@ struct SweepOpts {
   int live_only = 0;          // T-P loop: skip stores no later sweep reads
 };
 
+// FNV-1a over an argument block (zero-initialised structs: padding bytes are zero)
+template <typename T>
+uint64_t arg_hash(uint64_t h, const T& x) {
+  const unsigned char* b = reinterpret_cast<const unsigned char*>(&x);
+  for (size_t i = 0; i < sizeof(T); ++i) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+
 // One sweep: K1 -> reduce -> [RCCL all-gather] -> K4/K5 (+ next setup).  Asynchronous.
+// With c->dry it only appends the hash of every launch's arguments to c->keys and applies
+// the host-side state changes (temperature buffer swap), launching nothing.
 int run_sweep(frei_ctx* c, const SweepOpts& o) {
   const int ns = c->nL - 1;
   SweepArgs a{};
@@ -561,21 +585,28 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
         ((size_t)(kBlock / 64) * ns * 4 + (size_t)(kBlock / 64) * 2 * 4 * 72) * sizeof(double) +
                 (size_t)ns * sizeof(FastStepS) <= 48 * 1024)
       f.red_rows = 2;
-    if (Q > 1) {
-      nb_run = (int)((c->nlam + kBlock / Q - 1) / (kBlock / Q));
+    if (Q > 1) nb_run = (int)((c->nlam + kBlock / Q - 1) / (kBlock / Q));
+    if (c->keys) {
+      uint64_t h = arg_hash(1469598103934665603ull, f);
+      const int cfg[6] = {o.dir, Q, S_run, depth, (nan_check && !c->eff) ? 1 : 0, c->shared};
+      c->keys->push_back(arg_hash(h, cfg));
+    }
+    if (c->dry) {
+    } else if (Q > 1) {
       launch_sweep_group(o.dir, Q, f, nb_run, c->stream);
     } else {
       launch_sweep_fast(o.dir, S_run, depth, nan_check && !c->eff, c->shared != 0, f,
                         c->nblocks, c->stream);
     }
   } else {
-    launch_sweep(o.dir, a, c->nblocks, false, c->stream);
+    if (c->keys) c->keys->push_back(arg_hash(arg_hash(1469598103934665603ull, a), o.dir));
+    if (!c->dry) launch_sweep(o.dir, a, c->nblocks, false, c->stream);
   }
   HIP_TRY(hipGetLastError());
   if (c->timing) HIP_TRY(hipEventRecord(e1, c->stream));
   P2PPush push{};
   P2PWait wait{};
-  if (c->d_mbox) {   // P2P: the reduce kernel pushes, the update kernel waits (no host step)
+  if (c->d_mbox && !c->dry) {   // P2P: the reduce kernel pushes, the update kernel waits
     const uint64_t seq = ++c->p2p_seq;
     push.peers = c->d_peers;
     push.nranks = c->nranks;
@@ -595,6 +626,10 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   const bool fused = c->fused_update && c->n_atm == 1 && !c->comm &&
                      !(c->nranks > 1 && c->host_ag) &&
                      (2 * (size_t)c->nL + c->tnodes.size()) * sizeof(double) <= 32 * 1024;
+  if (!fused && c->dry) {   // not graph-replayable (the check in iterate() sees the marker)
+    if (c->keys) c->keys->push_back(0);
+    return 0;
+  }
   if (!fused) {
     const AtmStride bs = atm_stride(c);
     launch_reduce(c->d_part, nb_run, c->d_Fb, ns * 4, c->d_conv, o.force, c->stream,
@@ -666,7 +701,8 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     u.push = push;
     u.T_out = c->d_T_alt;
     u.done = c->d_done;
-    launch_update_fused(u, c->stream);
+    if (c->keys) c->keys->push_back(arg_hash(1469598103934665603ull, u));
+    if (!c->dry) launch_update_fused(u, c->stream);
     HIP_TRY(hipGetLastError());
     std::swap(c->d_T, c->d_T_alt);
     return 0;
@@ -674,6 +710,12 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   launch_update(u, c->stream, c->n_atm);
   HIP_TRY(hipGetLastError());
   return 0;
+}
+
+// A host upload overwrites the current temperatures, so the fused update's ping-pong can
+// restart from the same buffer (every run then issues identical launch arguments).
+void home_temperatures(frei_ctx* c) {
+  if (c->d_T != c->d_T_home) std::swap(c->d_T, c->d_T_alt);
 }
 
 int reset_loop_state(frei_ctx* c) {
@@ -725,7 +767,7 @@ bool ready(frei_ctx* c) { return c && c->grid_set; }
 const char* const kOptionNames[] = {"prefetch_depth", "shared", "shared_max_blocks",
                                     "precontract", "depth4_max_blocks", "pair_max_blocks",
                                     "quad_max_blocks", "red_rows", "red_stage", "group_q",
-                                    "fused_update", nullptr};
+                                    "fused_update", "graph", nullptr};
 int set_option(frei_ctx* c, const std::string& k, int v) {
   if (k == "prefetch_depth") c->prefetch_depth = v;
   else if (k == "shared") c->shared_mode = v < 0 ? -1 : (v ? 1 : 0);
@@ -738,6 +780,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "red_stage") c->red_stage = v != 0;
   else if (k == "group_q") c->group_q = (v == 1 || v == 2 || v == 4) ? v : 0;
   else if (k == "fused_update") c->fused_update = v != 0;
+  else if (k == "graph") c->use_graph = v != 0;
   else return fail("unknown option '" + k + "'");
   c->meta_dirty = true;
   return 0;
@@ -823,6 +866,7 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
       (rc = dalloc(&c->d_flips, NL * A)) || (rc = dalloc(&c->d_prev, NL * A)) ||
       (rc = dalloc(&c->d_ndiff, NL * A)) || (A > 1 && (rc = dalloc(&c->d_g, A))))
     return bail(rc);
+  c->d_T_home = c->d_T;
   if (hipHostMalloc((void**)&c->h_flag, 2 * sizeof(int)) != hipSuccess)
     return bail(fail("hipHostMalloc failed"));
   for (int k = 0; k < 2; ++k)
@@ -856,6 +900,8 @@ int frei_ctx_destroy(frei_ctx* c) {
     Rccl* r = rccl();
     if (r && r->commDestroy) r->commDestroy(c->comm);
   }
+  if (c->g_exec) (void)hipGraphExecDestroy(c->g_exec);
+  c->g_exec = nullptr;
   for (void* p : c->peer_mapped) (void)hipIpcCloseMemHandle(p);
   c->peer_mapped.clear();
   dfree(c->d_peers);
@@ -1157,6 +1203,7 @@ int frei_set_temperatures(frei_ctx* c, const double* T) {
   for (size_t l = 0; l < n; ++l)
     if (!(T[l] > 0)) return fail("temperatures must be positive");
   TRY(set_device(c));
+  home_temperatures(c);
   TRY(h2d(c->d_T, T, n, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return 0;
@@ -1210,6 +1257,7 @@ int frei_state_init(frei_ctx* c, const double* T_init) {
   if (!ready(c) || !T_init) return fail("context not ready or null T_init");
   TRY(set_device(c));
   TRY(build_meta(c));
+  home_temperatures(c);
   TRY(h2d(c->d_T, T_init, (size_t)c->nL * c->n_atm, c->stream));
   const size_t F = (size_t)c->nL * c->nlam * c->n_atm;
   HIP_TRY(hipMemsetAsync(c->d_Fu, 0, F * sizeof(double), c->stream));  // core.py:265-266
@@ -1220,7 +1268,7 @@ int frei_state_init(frei_ctx* c, const double* T_init) {
   return 0;
 }
 
-static int iterate(frei_ctx* c, int n, int nzc, double thr, double alpha, bool stop) {
+static int iterate_direct(frei_ctx* c, int n, int nzc, double thr, double alpha, bool stop) {
   for (int it = 0; it < n; ++it) {
     SweepOpts e;
     e.dir = kEmit;
@@ -1240,6 +1288,55 @@ static int iterate(frei_ctx* c, int n, int nzc, double thr, double alpha, bool s
   return 0;
 }
 
+// Graph replay applies when one iteration is two fused launches pairs on one rank with no
+// per-launch host work (no events, no exchange), i.e. when its kernel arguments repeat.
+static bool graph_ok(frei_ctx* c) {
+  return c->use_graph && c->graph_iters > 0 && !c->timing && c->fused_update && c->n_atm == 1 &&
+         c->nranks == 1 && !c->comm && !c->d_mbox;
+}
+
+static int iterate(frei_ctx* c, int n, int nzc, double thr, double alpha, bool stop) {
+  const int G = c->graph_iters;
+  if (!graph_ok(c) || n < G) return iterate_direct(c, n, nzc, thr, alpha, stop);
+  // the hashes of one iteration's launches as they would be issued now
+  std::vector<uint64_t> key;
+  c->keys = &key;
+  c->dry = true;
+  const int rc = iterate_direct(c, 1, nzc, thr, alpha, stop);
+  c->dry = false;
+  c->keys = nullptr;
+  TRY(rc);
+  // sweep, fused update, sweep, fused update (0: a launch that is not replayable)
+  const bool fused_only = key.size() == 4 && std::find(key.begin(), key.end(), 0ull) == key.end();
+  if (!fused_only) return iterate_direct(c, n, nzc, thr, alpha, stop);
+  if (!c->g_exec || key != c->g_key) {
+    if (c->g_exec) (void)hipGraphExecDestroy(c->g_exec);
+    c->g_exec = nullptr;
+    c->g_key.clear();
+    hipGraph_t g = nullptr;
+    HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    const int rc2 = iterate_direct(c, G, nzc, thr, alpha, stop);
+    const hipError_t e = hipStreamEndCapture(c->stream, &g);
+    TRY(rc2);
+    if (e != hipSuccess) return fail(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+    const hipError_t ei = hipGraphInstantiate(&c->g_exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ei != hipSuccess) {
+      c->g_exec = nullptr;
+      return fail(std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
+    }
+    c->g_key = key;
+    ++c->g_captures;
+    // the capture swapped the temperature buffers 2 G times: an even count, back in place
+  }
+  int done = 0;
+  for (; done + G <= n; done += G) {
+    HIP_TRY(hipGraphLaunch(c->g_exec, c->stream));
+    ++c->g_replays;
+  }
+  return iterate_direct(c, n - done, nzc, thr, alpha, stop);
+}
+
 int frei_iterate(frei_ctx* c, int n, int n_zero_crossings, double convergence_dT,
                  double alpha) {
   if (!ready(c)) return fail("context not ready");
@@ -1247,6 +1344,13 @@ int frei_iterate(frei_ctx* c, int n, int n_zero_crossings, double convergence_dT
   TRY(ensure_hist(c, 1));
   const bool stop = n_zero_crossings >= 0;
   return iterate(c, n, stop ? n_zero_crossings : 0x7fffffff, convergence_dT, alpha, stop);
+}
+
+int frei_graph_info(frei_ctx* c, int* captures, int* replays) {
+  if (!c) return fail("null argument");
+  if (captures) *captures = c->g_captures;
+  if (replays) *replays = c->g_replays;
+  return 0;
 }
 
 int frei_synchronize(frei_ctx* c) {

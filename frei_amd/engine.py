@@ -297,6 +297,12 @@ class Engine:
         """Tuning knob of include/frei_hip.h frei_set_option (e.g. "precontract", 0)."""
         N.check(N.lib().frei_set_option(self._ctx, name.encode(), int(value)))
 
+    def graph_info(self):
+        """(captures, replays) of the hipGraph T-P iteration replay (frei_graph_info)."""
+        cap, rep = ctypes.c_int(0), ctypes.c_int(0)
+        N.check(N.lib().frei_graph_info(self._ctx, ctypes.byref(cap), ctypes.byref(rep)))
+        return cap.value, rep.value
+
     def setup_timing(self):
         """Milliseconds of the last one-time metadata build by phase (frei_setup_timing)."""
         ms = np.zeros(5)

@@ -224,8 +224,13 @@ int frei_ctx_path(frei_ctx* ctx, int* flags);
  * "shared_max_blocks", "pair_max_blocks", "quad_max_blocks", "depth4_max_blocks",
  * "red_rows", "red_stage" (take effect at the next metadata build), "fused_update" (1: one
  * launch for the partial-sum reduction and the T update when the exchange is local or P2P;
- * 0: two kernels; bitwise identical results; takes effect at the next sweep). */
+ * 0: two kernels; bitwise identical results; takes effect at the next sweep), "graph" (1:
+ * replay T-P iterations from a captured hipGraph; 0, the default: launch kernel by kernel). */
 int frei_set_option(frei_ctx* ctx, const char* name, int value);
+/* With the "graph" option on (default off), T-P iterations (frei_iterate, frei_run) are
+ * replayed from a captured hipGraph of a few iterations when one rank runs with timing off:
+ * the number of captures and of graph launches so far. */
+int frei_graph_info(frei_ctx* ctx, int* captures, int* replays);
 /* Host wall-clock milliseconds of the last metadata build (the one-time setup before the
  * first sweep after tables/mmr change), by phase: [0] per-(species, layer) brackets on the
  * host, [1] metadata uploads, [2] contracted-table allocation, [3] its zero fill, [4] the K3

@@ -103,3 +103,40 @@ def test_fused_update_is_bitwise_identical_to_two_kernels(fa, name, opts):
             _same(a[key][what], b[key][what], f"{name} {key} {what}")
     _same(a["iterate"], b["iterate"], f"{name} iterate T")
     assert 1 < a["run"]["n_iter"] <= 80
+
+
+@pytest.mark.parametrize("name,opts", [("contracted", {}), ("per_species", {"precontract": 0}),
+                                       ("contracted", {"group_q": 2})])
+def test_graph_replay_is_bitwise_identical_to_launches(fa, name, opts):
+    """T-P iterations replayed from a captured hipGraph (frei_iterate / frei_run) against
+    kernel-by-kernel launches: same kernels, same arguments, so bit-identical state; the graph
+    is captured once and reused while the arguments repeat."""
+    lam, p, T0, tabs, mmr = _case(fa, name)
+    eng = fa.Engine(lam, p, tabs, mmr=mmr)
+    out = {}
+    try:
+        for k, v in opts.items():
+            eng.set_option(k, v)
+        for graph in (1, 0):
+            eng.set_option("graph", graph)
+            r = {}
+            r["run"] = eng.run(T0, n_timesteps=80)
+            r["run_again"] = eng.run(T0, n_timesteps=80)
+            eng.state_init(T0)
+            eng.iterate(9, n_zero_crossings=10 ** 6, convergence_dT=-1.0)   # 2 replays + 1
+            eng.synchronize()
+            r["iterate"] = eng.get_temperatures()
+            out[graph] = r
+            if graph:
+                cap, rep = eng.graph_info()
+                # run's stop/threshold arguments differ from iterate's: two graphs in total
+                assert cap == 2 and rep >= 4, (cap, rep)
+    finally:
+        eng.close()
+    a, b = out[1], out[0]
+    for key in ("run", "run_again"):
+        assert a[key]["n_iter"] == b[key]["n_iter"]
+        for what in ("final_T", "temp_hist", "spectrum", "dtaus"):
+            _same(a[key][what], b[key][what], f"{name} {key} {what}")
+    _same(a["run"]["final_T"], a["run_again"]["final_T"], "graph reuse")
+    _same(a["iterate"], b["iterate"], f"{name} iterate T")
