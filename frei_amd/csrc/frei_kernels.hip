@@ -781,20 +781,30 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   struct Pre {
     double vlo, vhi, stale, wl, wh, dm, T;
   };
+  // per-lane running addresses, advanced by Q steps per load: this lane's stale row (emit:
+  // F_down row k + 2; absorb: F_up row nL - 2 - k) and its table column
+  const double* tabj = tab + j;
+  const double* ftoaj = a.ftoa + j;
+  const int64_t sstep = (DIR == kEmit ? (int64_t)Q : -(int64_t)Q) * nl;
+  const double* pst = (DIR == kEmit) ? Fd + (int64_t)(q + 2) * nl + j
+                                     : Fu + (int64_t)(nL - 2 - q) * nl + j;
+  int kl = q;                        // this lane's step of the next load
   auto load = [&](int g, Pre& P) {
-    const int k = clampk(Q * g + q);
-    const FastStepS& st = sp[k];
-    const double* r = tab + st.off + j;
+    (void)g;
+    const FastStepS& st = sp[clampk(kl)];
+    const double* r = tabj + st.off;
     P.wl = st.wlo;
     P.wh = st.whi;
     P.dm = st.dm;
     P.T = DIR == kEmit ? st.T2 : st.T1;
     P.vlo = stream_load(r);
     P.vhi = stream_load(r + a.pitch);
-    const int layer = step_layer(DIR, k, nL);
-    const double* src = (DIR == kEmit) ? (is_top(k) ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
-                                       : Fu + (int64_t)layer * nl;
-    P.stale = src[j];
+    // emit's top step reads F_TOA; past the last step (dummy groups) any valid row serves
+    const double* src = (DIR == kEmit) ? (kl >= ns - 1 ? ftoaj : pst)
+                                       : (kl >= ns ? Fu + j : pst);
+    P.stale = *src;
+    pst += sstep;
+    kl += Q;
   };
   double carry, carryB;
   {
@@ -827,26 +837,12 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     // (B1, B2) of its steps in order (emit: B2 is new and becomes the next B1; absorb: B1 is
     // new and becomes the next B2; emit's top step keeps B2 = B1)
     const double X = planck(c1, lk, Tnew, ek);
-    double Xr[Q], Bn[Q];
-    Xr[0] = from_lane<Q, 0>(X);
-    Xr[1] = from_lane<Q, 1>(X);
-    if constexpr (Q == 4) {
-      Xr[2] = from_lane<Q, 2>(X);
-      Xr[3] = from_lane<Q, 3>(X);
-    }
-    double prev = carryB;
-#pragma unroll
-    for (int r = 0; r < Q; ++r) {
-      const bool top = is_top(Q * g + r);
-      Bn[r] = (DIR == kEmit && top) ? prev : Xr[r];
-      prev = Bn[r];
-    }
-    double before = carryB, mine = Bn[0];
-#pragma unroll
-    for (int r = 1; r < Q; ++r) {
-      before = (q == r) ? Bn[r - 1] : before;
-      mine = (q == r) ? Bn[r] : mine;
-    }
+    // the step before this lane's holds the lane before it in the group (quad_perm
+    // [0,0,2,2] for Q = 2, [0,0,1,2] for Q = 4), the group's first step the carried value;
+    // emit's top step keeps B2 = B1 (it is the last step, so no later step reads it)
+    const double Xp = dpp_bcast<Q == 2 ? 0xA0 : 0x90>(X);
+    const double before = (q == 0) ? carryB : Xp;
+    const double mine = (DIR == kEmit && is_top(k)) ? before : X;
     if (DIR == kEmit) {
       A.B1 = before;
       A.B2 = mine;
@@ -854,7 +850,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
       A.B2 = before;
       A.B1 = mine;
     }
-    carryB = Bn[Q - 1];
+    carryB = from_lane<Q, Q - 1>(mine);
   };
   // This lane's flux / dtau row pointers for its step of the current group: Q rows on per
   // group (up for emit, down for absorb), so the stores need no per-step row arithmetic.
@@ -933,7 +929,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     }
   };
   const int ng = (ns + Q - 1) / Q;
-  Pre pa, pb;                      // two groups in flight
+  Pre pa, pb;                      // two groups in flight (4: measured no faster)
   load(0, pa);
   load(1, pb);
   for (int g = 0; g < ng; g += 2) {
