@@ -35,13 +35,25 @@ def _tables():
     return w, tabs
 
 
+def _chem(fa, w):
+    """T-dependent chemistry for the C3 species (mmr on (T, p) nodes around each species'
+    median mixing ratio: half the species fall with T, half rise), re-interpolated on the
+    device before every sweep; the sweep keeps the per-species sum."""
+    cT = np.linspace(300.0, 4000.0, 14)
+    cp = np.logspace(-7, 3, 9)
+    x = np.tanh((cT[:, None] - 1500.0) / 400.0) + 0.05 * np.log10(cp)[None, :]
+    vals = {n: float(np.median(w["mmr"][s])) * 10 ** (0.5 * (-1) ** s * x)
+            for s, n in enumerate(w["names"])}
+    return fa.ChemistryTable(vals, cT, cp)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
 
 
-def _rank(rank, world, port, transport, q):
+def _rank(rank, world, port, transport, q, chem=False):
     try:
         from frei_amd.distributed import host_comm, p2p_comm, partition
         from frei_amd.engine import Engine
@@ -52,7 +64,12 @@ def _rank(rank, world, port, transport, q):
         w, tabs = _tables()
         lo, hi = partition(w["lam"].size, world, rank)
         comm = (p2p_comm if transport == "p2p" else host_comm)(rdzv)
-        eng = Engine(w["lam"], w["p"], tabs, mmr=w["mmr"], device=0, lam_slice=(lo, hi),
+        if chem:
+            import frei_amd as fa
+            mmr = _chem(fa, w)
+        else:
+            mmr = w["mmr"]
+        eng = Engine(w["lam"], w["p"], tabs, mmr=mmr, device=0, lam_slice=(lo, hi),
                      comm=comm)
         out = eng.run(w["T0"], **RUN)
         eng.close()
@@ -109,5 +126,37 @@ def test_c4_two_rank_lambda_shards_match_unsharded(unsharded, transport):
     assert np.array_equal(res[0][4], res[1][4])            # bitwise-identical T on every rank
     assert rel(res[0][4], ref["final_T"]) < 1e-12
     assert res[0][2] == res[1][1] and res[1][2] == w["lam"].size
+    spec = np.concatenate([res[0][5], res[1][5]])
+    assert rel(spec, ref["spectrum"]) < 1e-10
+
+
+def test_c4_chemistry_two_rank_p2p_matches_unsharded():
+    """C4 with T-dependent chemistry: the per-species sweep with mixing ratios re-evaluated
+    at every layer's current T each sweep, to convergence, unsharded and as two P2P ranks."""
+    import frei_amd as fa
+    from frei_amd.engine import Engine
+    w, tabs = _tables()
+    eng = Engine(w["lam"], w["p"], tabs, mmr=_chem(fa, w))
+    try:
+        assert not eng.path()["contracted"]
+        ref = eng.run(w["T0"], **RUN)
+    finally:
+        eng.close()
+    assert 1 < ref["n_iter"] < RUN["n_timesteps"], ref["n_iter"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, "p2p", q, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in res:
+        assert r[6] is None, f"rank {r[0]}: {r[6]}"
+    assert res[0][3] == res[1][3] == ref["n_iter"]
+    assert np.array_equal(res[0][4], res[1][4])
+    assert rel(res[0][4], ref["final_T"]) < 1e-12
     spec = np.concatenate([res[0][5], res[1][5]])
     assert rel(spec, ref["spectrum"]) < 1e-10
