@@ -286,6 +286,8 @@ def sweep_kernel_time(eng, n_iter):
 def main():
     _reserve_stdout()
     a = parse()
+    # a peer that never publishes its sums fails the run after this long instead of 30 s
+    os.environ.setdefault("FREI_P2P_TIMEOUT_S", "10")
     d = Dist(a.gpus)
     from frei_amd import _native as N
     from frei_amd.engine import partition

@@ -1030,7 +1030,9 @@ __device__ __forceinline__ double p2p_take(const P2PWait& w, int r, int64_t idx,
   const uint64_t* fl =
       reinterpret_cast<const uint64_t*>(w.mbox) + mbox_flag(par, r, w.nranks, w.n) + idx;
   while (__hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != w.seq) {
-    if (wall_clock64() - t0 > w.timeout_ticks) {
+    // after one timeout every later wait gives up at once (the run is already failed)
+    if (wall_clock64() - t0 > w.timeout_ticks ||
+        __hip_atomic_load(w.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
       __hip_atomic_store(w.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
