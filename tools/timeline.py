@@ -1,6 +1,9 @@
 """Per-sweep timeline of the T-P loop from a rocprofv3 kernel trace.
 
-    python tools/timeline.py path/to/run_kernel_trace.csv
+    python tools/timeline.py path/to/run_kernel_trace.csv [SWEEP_GRID_X]
+
+SWEEP_GRID_X keeps only the sweeps of that grid size (e.g. 500224 for the 500k one-lane sweep,
+leaving out the batched and per-atmosphere legs of a full bench run).
 
 For every sweep -> reduce -> (all-gather) -> update cycle (or sweep -> fused update) it attributes the kernel durations
 and the idle gaps between consecutive kernels (end of one to start of the next), then
@@ -21,11 +24,13 @@ def kind(name):
     return None
 
 
-def main(path):
+def main(path, grid=None):
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
             k = kind(r["Kernel_Name"])
+            if k == "sweep" and grid is not None and r["Grid_Size_X"] != grid:
+                k = None
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k,
                          r["Kernel_Name"][:60]))
     rows.sort()
@@ -60,4 +65,4 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
