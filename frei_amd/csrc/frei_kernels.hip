@@ -1219,37 +1219,53 @@ __global__ void setup_kernel(SetupArgs u, int dir) {
 }
 
 // ---------------------------------------------------------------- K4/K5: update
-__device__ double layer_dT(const double* Fb, double T1, double T2, double p1, double p2,
-                           double lnp, double g, double m_bar, double alpha) {
+// layer_dT in two parts: everything that depends only on the layer's T and p (formed while
+// the sweep's partial sums are still being loaded), then the flux-dependent tail.  The same
+// operations in the same order as one expression: bit-identical.
+struct LayerPre {
+  double dz, cp, dF_conv, dt_rad, dt_conv, rho0, cp0;
+  bool conv;
+};
+
+__device__ __forceinline__ LayerPre layer_pre(double T1, double T2, double p1, double p2,
+                                              double lnp, double g, double m_bar,
+                                              double alpha) {
+  LayerPre r;
   // div_bol_net_flux (twostream.py:190-205); lnp = log(p1 / p2) (log_ratio_kernel)
-  const double dF_rad = (Fb[0] - Fb[1]) - (Fb[2] - Fb[3]);
-  const double dz = (kKB * T1) / (m_bar * g) * lnp;                   // :180-187
-  const double cp = (2 + 5) / (2 * m_bar) * kKB;                      // :220-224
-  const double rho = ((p1 - p2) / g) / dz;                            // :234-238
-  const double dg = (T1 - T2) / dz - g / cp;                          // :241-266
-  double dF_conv = 0.0;                                               // :273-287
-  if (dg > 0) {
+  r.dz = (kKB * T1) / (m_bar * g) * lnp;                         // :180-187
+  r.cp = (2 + 5) / (2 * m_bar) * kKB;                            // :220-224
+  const double rho = ((p1 - p2) / g) / r.dz;                     // :234-238
+  const double dg = (T1 - T2) / r.dz - g / r.cp;                 // :241-266
+  r.conv = dg > 0;
+  r.dF_conv = 0.0;                                               // :273-287
+  r.dt_conv = 0.0;
+  if (r.conv) {
     const double lmix = alpha * kKB * T1 / (m_bar * g);
-    dF_conv = rho * cp * (lmix * lmix) * sqrt(g / T1) * pow(dg, 1.5);
+    r.dF_conv = rho * r.cp * (lmix * lmix) * sqrt(g / T1) * pow(dg, 1.5);
+    r.dt_conv = sqrt(T1 / g / dg);
   }
-  const double div = (dF_rad + dF_conv) / dz;
-  // delta_t_i (:23-43)
-  const double x = div * dz;
-  const double f = (x != 0) ? 1e5 / pow(fabs(x), 0.9) : 1.0;
-  const double dt_rad = cp * p1 / kSigmaSB / g / pow(T1, 3.0);
-  double dt;
-  if (dg > 0) {
-    const double dt_conv = sqrt(T1 / g / dg);
-    dt = f * fmin(dt_rad, dt_conv);
-  } else {
-    dt = f * dt_rad;
-  }
+  // delta_t_i (:23-43): the radiative timescale
+  r.dt_rad = r.cp * p1 / kSigmaSB / g / pow(T1, 3.0);
   // delta_temperature with the default m_bar (:208-217, Q7)
   const double m0 = kMbarDefault;
   const double dz0 = (kKB * T1) / (m0 * g) * lnp;
-  const double rho0 = ((p1 - p2) / g) / dz0;
-  const double cp0 = (2 + 5) / (2 * m0) * kKB;
-  return 1 / rho0 / cp0 * div * dt;
+  r.rho0 = ((p1 - p2) / g) / dz0;
+  r.cp0 = (2 + 5) / (2 * m0) * kKB;
+  return r;
+}
+
+__device__ __forceinline__ double layer_dT_post(const double* Fb, const LayerPre& r) {
+  const double dF_rad = (Fb[0] - Fb[1]) - (Fb[2] - Fb[3]);
+  const double div = (dF_rad + r.dF_conv) / r.dz;
+  const double x = div * r.dz;
+  const double f = (x != 0) ? 1e5 / pow(fabs(x), 0.9) : 1.0;
+  const double dt = r.conv ? f * fmin(r.dt_rad, r.dt_conv) : f * r.dt_rad;
+  return 1 / r.rho0 / r.cp0 * div * dt;
+}
+
+__device__ double layer_dT(const double* Fb, double T1, double T2, double p1, double p2,
+                           double lnp, double g, double m_bar, double alpha) {
+  return layer_dT_post(Fb, layer_pre(T1, T2, p1, p2, lnp, g, m_bar, alpha));
 }
 
 // One workgroup.  Phase 0 issues every global read the kernel needs at once (T, p, sorted
@@ -1446,6 +1462,9 @@ __global__ __launch_bounds__(256) void update_fused_kernel(UpdateArgs a) {
   const double T2 = top ? T1 : rT2;
   const double p2 = top ? a.su.p_top2 : rp2;
   const double Tl = T1;              // lanes with (tid & 1) == 0: layer l
+  // dT's flux-independent part while the partial sums load (lanes 0, 1: layers l, l + 1)
+  LayerPre pre{};
+  if (tid < 2 && kd >= 0) pre = layer_pre(T1, T2, p1, p2, lnp, a.su.g, a.m_bar, a.alpha);
   if (!a.force && conv) {    // converged: carry T into the output buffer
     if (tid == 0) a.T_out[l] = Tl;
     return;
@@ -1513,9 +1532,9 @@ __global__ __launch_bounds__(256) void update_fused_kernel(UpdateArgs a) {
     double d = 0.0;
     if (tid < 2 && kd >= 0) {
 #ifdef FREI_UPD_NODT  // diagnostic ablation build
-      d = 1e-3 * (F[0] - F[1]) + T2 * 1e-9 + p2 * 1e-20 + lnp * 0;
+      d = 1e-3 * (F[0] - F[1]) + T2 * 1e-9 + p2 * 1e-20 + lnp * 0 + pre.dz * 0;
 #else
-      d = layer_dT(F, T1, T2, p1, p2, lnp, a.su.g, a.m_bar, a.alpha);
+      d = layer_dT_post(F, pre);
 #endif
       sTn[li] = T1 - d;
     }
