@@ -510,7 +510,9 @@ uint64_t arg_hash(uint64_t h, const T& x) {
   return h;
 }
 
-// One sweep: K1 -> reduce -> [RCCL all-gather] -> K4/K5 (+ next setup).  Asynchronous.
+// One sweep: K1 -> fused reduce + update (+ next setup; P2P exchange inside), or K1 ->
+// reduce -> [RCCL / host all-gather] -> K4/K5 (batched contexts, RCCL, host hook,
+// fused_update 0).  Asynchronous.
 // With c->dry it only appends the hash of every launch's arguments to c->keys and applies
 // the host-side state changes (temperature buffer swap), launching nothing.
 int run_sweep(frei_ctx* c, const SweepOpts& o) {
@@ -606,7 +608,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   if (c->timing) HIP_TRY(hipEventRecord(e1, c->stream));
   P2PPush push{};
   P2PWait wait{};
-  if (c->d_mbox && !c->dry) {   // P2P: the reduce kernel pushes, the update kernel waits
+  if (c->d_mbox && !c->dry) {   // P2P: each rank's sums are pushed and waited for on device
     const uint64_t seq = ++c->p2p_seq;
     push.peers = c->d_peers;
     push.nranks = c->nranks;
