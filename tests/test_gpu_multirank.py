@@ -79,3 +79,78 @@ def test_ranks_on_one_gpu_match_single_rank(transport, world):
     assert np.max(np.abs(res[0][4] - ref["final_T"]) / ref["final_T"]) < 1e-11
     spec = np.concatenate([r[3] for r in res])
     assert np.max(np.abs(spec - ref["spectrum"]) / np.abs(ref["spectrum"])) < 1e-10
+
+
+def _silent_worker(rank, world, port, q, hold_s):
+    """Joins the P2P exchange (handles, mailbox mapping, handshake) and then never sweeps:
+    a peer that stops publishing its sums.  Keeps its mailbox alive while the other rank
+    runs into the timeout."""
+    try:
+        import time
+        from frei_amd.distributed import p2p_comm, partition
+        from frei_amd.engine import Engine
+        from frei_amd.rendezvous import Rendezvous
+        from tests.mp_helpers import offset_device_allocations
+        offset_device_allocations(rank)
+        rdzv = Rendezvous(world, rank, addr=("127.0.0.1", port), timeout=120)
+        grid, op = _problem()
+        lo, hi = partition(grid.lam.size, world, rank)
+        eng = Engine(grid.lam, grid.pressures, op, device=0, lam_slice=(lo, hi),
+                     comm=p2p_comm(rdzv))
+        rdzv.barrier()                    # both engines exist
+        rdzv.barrier()                    # rank 0 has seen its error
+        time.sleep(hold_s)
+        eng.close()
+        rdzv.close()
+        q.put((rank, None))
+    except Exception as e:
+        q.put((rank, repr(e)))
+
+
+def _timeout_worker(rank, world, port, q):
+    try:
+        import time
+        from frei_amd.distributed import p2p_comm, partition
+        from frei_amd.engine import Engine
+        from frei_amd.rendezvous import Rendezvous
+        rdzv = Rendezvous(world, rank, addr=("127.0.0.1", port), timeout=120)
+        grid, op = _problem()
+        lo, hi = partition(grid.lam.size, world, rank)
+        eng = Engine(grid.lam, grid.pressures, op, device=0, lam_slice=(lo, hi),
+                     comm=p2p_comm(rdzv))
+        rdzv.barrier()
+        t0 = time.monotonic()
+        err = None
+        try:
+            eng.run(grid.init_temperatures, n_timesteps=20)
+        except RuntimeError as e:
+            err = str(e)
+        dt = time.monotonic() - t0
+        rdzv.barrier()
+        eng.close()
+        rdzv.close()
+        q.put((rank, (err, dt)))
+    except Exception as e:
+        q.put((rank, repr(e)))
+
+
+def test_p2p_missing_peer_fails_with_timeout_not_hang(monkeypatch):
+    """A peer that joined the exchange but never publishes: the waiting rank's run ends with
+    the engine's timeout error after about FREI_P2P_TIMEOUT_S (every later wait gives up at
+    once), instead of hanging the GPU."""
+    monkeypatch.setenv("FREI_P2P_TIMEOUT_S", "2")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timeout_worker, args=(0, 2, port, q)),
+             ctx.Process(target=_silent_worker, args=(1, 2, port, q, 1.0))]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] is None, res[1]
+    err, dt = res[0]
+    assert err is not None and "timed out" in err, res[0]
+    assert dt < 60, dt
