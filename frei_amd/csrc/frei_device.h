@@ -36,7 +36,7 @@ __host__ __device__ inline int layer_step(int dir, int i, int nL) {
 
 // Per sweep step, wave-uniform.
 struct StepP {
-  double T1, T2;  // K
+  double iT1, iT2;  // 1 / T of the step's two layers, K^-1 (the Planck exponent hc/(lam k) * (1/T))
   double dm;      // (p1 - p2) / g, g cm^-2 (twostream.py:227-231)
   int32_t layer;  // i
   int32_t top;    // emit top layer: F_2_down = F_TOA, F_2_up not stored (Q3)
@@ -47,7 +47,7 @@ struct StepP {
 // two T-bracket rows per species, row_hi = row_lo + n_lam (T axis stored ascending).
 constexpr int kMaxFastS = 8;
 struct FastStep {
-  double T1, T2, dm;
+  double iT1, iT2, dm;     // 1 / T of the step's two layers (K^-1), (p1 - p2) / g
   int32_t layer, top;
   double wlo[kMaxFastS], whi[kMaxFastS], mmr[kMaxFastS];
   int64_t off[kMaxFastS];  // element offset of the T_lo row in species s's table
@@ -57,7 +57,7 @@ struct FastStep {
 // usual case: tables binned onto the grid), so one row offset and one weight pair serve all
 // species; 15 uniform values per step fit SGPRs and are prefetched with the table rows.
 struct FastStepS {
-  double T1, T2, dm, wlo, whi;
+  double iT1, iT2, dm, wlo, whi;   // 1 / T of the two layers (K^-1), ...
   int64_t off;             // element offset of the T_lo row (same in every species table)
   int32_t layer, top;
   double mmr[kMaxFastS];
@@ -258,7 +258,7 @@ struct FastArgs {
   int64_t pitch;           // table row pitch (elements), even
   int n_steps, force;
   int live_only;           // skip flux stores no later sweep reads (T-P loop only)
-  const double *c1, *lk, *sig, *wtr, *ftoa;
+  const double *c1, *hcl, *sig, *wtr, *ftoa;   // hcl = hc / (lam k_B)
   const double* tab[kMaxFastS];
   const FastStep* steps;
   const FastStepS* ssteps;
@@ -277,7 +277,7 @@ struct SweepArgs {
   int64_t n_lam;
   int n_steps, n_species, force;
   int live_only;
-  const double *c1, *lk, *sig, *wtr, *ftoa;
+  const double *c1, *hcl, *sig, *wtr, *ftoa;   // hcl = hc / (lam k_B)
   const StepP* steps;
   const TermP* terms;
   double* F_up;

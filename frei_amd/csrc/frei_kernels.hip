@@ -23,12 +23,15 @@
 namespace frei {
 
 // ---------------------------------------------------------------- device math
-__device__ __forceinline__ double planck(double c1, double lk, double T) {
-  // twostream.py:64-67: 2hc^2/lam^5 / expm1(hc / (lam k T))
+// twostream.py:64-67: 2hc^2/lam^5 / expm1(hc / (lam k T)).  The exponent is formed as
+// (hc / (lam k)) * (1 / T) — a per-wavelength constant (host) times a per-layer one (the step
+// record) — instead of one division per update: within 1.5 ulp of the reference's
+// hc / ((lam k) T), which moves spectra and T by < 1e-13.
+__device__ __forceinline__ double planck(double c1, double hcl, double iT) {
 #ifdef FREI_MEMONLY
-  return c1 * lk * T;
+  return c1 * hcl * iT;
 #else
-  return fm::div_big(c1, fm::expm1(fm::div(kHC, lk * T)));
+  return fm::div_big(c1, fm::expm1(hcl * iT));
 #endif
 }
 
@@ -42,15 +45,16 @@ __device__ __forceinline__ double planck(double c1, double lk, double T) {
 // range-select-free expm1 for exponents <= 600 and an IEEE fallback branch (execz-skipped)
 // for the rare lanes above — cold layers at short wavelengths, where expm1 passes 2^865 and
 // the guard-free division could lose the denormal quotient.
-__device__ __forceinline__ double planck(double c1, double lk, double T, const fm::Expm1Reg& k) {
+__device__ __forceinline__ double planck(double c1, double hcl, double iT,
+                                        const fm::Expm1Reg& k) {
 #if FREI_EXPM1_VREG && !defined(FREI_MEMONLY)
-  const double x = fm::div(kHC, lk * T);
+  const double x = hcl * iT;
   double B = fm::div(c1, fm::expm1_mid(x < 600.0 ? x : 600.0, k));
   if (__builtin_expect(!(x <= 600.0), 0)) B = c1 / fm::expm1(x, k);
   return B;
 #else
   (void)k;
-  return planck(c1, lk, T);
+  return planck(c1, hcl, iT);
 #endif
 }
 
@@ -259,7 +263,7 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
   const int64_t j0 = (int64_t)blockIdx.x * kBlock + tid;
   const bool act = j0 < nl;
   const int64_t j = act ? j0 : nl - 1;
-  const double c1 = a.c1[j], lk = a.lk[j], sig = a.sig[j];
+  const double c1 = a.c1[j], hcl = a.hcl[j], sig = a.sig[j];
   const double wt = act ? a.wtr[j] : 0.0;
   double* __restrict__ Fu = a.F_up;
   double* __restrict__ Fd = a.F_down;
@@ -271,10 +275,10 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     const StepP s0 = a.steps[0];
     if (DIR == kEmit) {  // fresh F_up carried upward (twostream.py:383)
       carry = Fu[(int64_t)s0.layer * nl + j];
-      Bc = planck(c1, lk, s0.T1);
+      Bc = planck(c1, hcl, s0.iT1);
     } else {             // fresh F_down carried downward (twostream.py:511)
       carry = Fd[(int64_t)(s0.layer + 1) * nl + j];
-      Bc = planck(c1, lk, s0.T2);
+      Bc = planck(c1, hcl, s0.iT2);
     }
   }
   for (int k = 0; k < ns; ++k) {
@@ -286,12 +290,12 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
     double B1, B2, F1u, F2d;
     if (DIR == kEmit) {
       B1 = Bc;
-      B2 = sp.top ? Bc : planck(c1, lk, sp.T2);
+      B2 = sp.top ? Bc : planck(c1, hcl, sp.iT2);
       F1u = carry;
       F2d = sp.top ? a.ftoa[j] : Fd[(int64_t)(i + 1) * nl + j];  // stale (Q2, Q3)
     } else {
       B2 = Bc;
-      B1 = planck(c1, lk, sp.T1);
+      B1 = planck(c1, hcl, sp.iT1);
       F2d = carry;
       F1u = Fu[(int64_t)i * nl + j];                               // stale (Q2)
     }
@@ -478,7 +482,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   const int64_t j0 = (int64_t)blockIdx.x * kBlock + tid;
   const bool act = j0 < nl;
   const int64_t j = act ? j0 : nl - 1;
-  const double c1 = a.c1[j], lk = a.lk[j], sig = a.sig[j];
+  const double c1 = a.c1[j], hcl = a.hcl[j], sig = a.sig[j];
   const double wt = act ? a.wtr[j] : 0.0;
   const int ns = a.n_steps;
   const fm::Expm1Reg ek = fm::expm1_regs();
@@ -534,18 +538,18 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   auto coef = [&](int k, double (&v)[2 * S], double& stale, double Bprev, StepCoef& c,
                   PreCoef& pc) {
     const int kk = k < ns ? k : ns - 1;  // the last pair of a PD = 2 loop may be a dummy
-    double T1, T2, dm;
+    double iT1, iT2, dm;   // inverse temperatures of the step's layers
     if constexpr (SH) {
       c.layer = layer_of(kk);
       c.top = top_of(kk);
-      T1 = UNIV(sp[kk].T1);
-      T2 = UNIV(sp[kk].T2);
+      iT1 = UNIV(sp[kk].iT1);
+      iT2 = UNIV(sp[kk].iT2);
       dm = UNIV(sp[kk].dm);
     } else {
       c.layer = layer_of(kk);
       c.top = top_of(kk);
-      T1 = st[kk].T1;
-      T2 = st[kk].T2;
+      iT1 = st[kk].iT1;
+      iT2 = st[kk].iT2;
       dm = st[kk].dm;
     }
     double tot = 0.0;
@@ -574,11 +578,11 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     double B1, B2;
     if (DIR == kEmit) {
       B1 = Bprev;
-      B2 = c.top ? Bprev : planck(c1, lk, T2, ek);
+      B2 = c.top ? Bprev : planck(c1, hcl, iT2, ek);
       c.Bnext = B2;
     } else {
       B2 = Bprev;
-      B1 = planck(c1, lk, T1, ek);
+      B1 = planck(c1, hcl, iT1, ek);
       c.Bnext = B1;
     }
     pc.w0 = w0;
@@ -654,13 +658,13 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   double Bc;
   {
     const int l0 = SH ? sp[0].layer : st[0].layer;
-    const double T10 = SH ? sp[0].T1 : st[0].T1, T20 = SH ? sp[0].T2 : st[0].T2;
+    const double iT10 = SH ? sp[0].iT1 : st[0].iT1, iT20 = SH ? sp[0].iT2 : st[0].iT2;
     if (DIR == kEmit) {
       carry = Fu[(int64_t)l0 * nl + j];
-      Bc = planck(c1, lk, T10, ek);
+      Bc = planck(c1, hcl, iT10, ek);
     } else {
       carry = Fd[(int64_t)(l0 + 1) * nl + j];
-      Bc = planck(c1, lk, T20, ek);
+      Bc = planck(c1, hcl, iT20, ek);
     }
   }
   // PD steps in flight: their loads are issued PD steps ahead, their coefficients form one
@@ -758,7 +762,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   const int64_t j0 = (int64_t)blockIdx.x * (kBlock / Q) + wv * (64 / Q) + lane / Q;
   const bool act = j0 < nl;
   const int64_t j = act ? j0 : nl - 1;
-  const double c1 = a.c1[j], lk = a.lk[j], sig = a.sig[j];
+  const double c1 = a.c1[j], hcl = a.hcl[j], sig = a.sig[j];
   const double wt = act ? a.wtr[j] : 0.0;
   const int ns = a.n_steps;
   const fm::Expm1Reg ek = fm::expm1_regs();
@@ -779,7 +783,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   // Everything group g's phase A reads, issued together one group ahead: the LDS step
   // parameters with the table rows and the stale flux (their latency overlaps).
   struct Pre {
-    double vlo, vhi, stale, wl, wh, dm, T;
+    double vlo, vhi, stale, wl, wh, dm, iT;
   };
   // per-lane running addresses, advanced by Q steps per load: this lane's stale row (emit:
   // F_down row k + 2; absorb: F_up row nL - 2 - k) and its table column
@@ -796,7 +800,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     P.wl = st.wlo;
     P.wh = st.whi;
     P.dm = st.dm;
-    P.T = DIR == kEmit ? st.T2 : st.T1;
+    P.iT = DIR == kEmit ? st.iT2 : st.iT1;
     P.vlo = stream_load(r);
     P.vhi = stream_load(r + a.pitch);
     // emit's top step reads F_TOA; past the last step (dummy groups) any valid row serves
@@ -811,10 +815,10 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     const int l0 = sp[0].layer;
     if (DIR == kEmit) {
       carry = Fu[(int64_t)l0 * nl + j];
-      carryB = planck(c1, lk, sp[0].T1, ek);
+      carryB = planck(c1, hcl, sp[0].iT1, ek);
     } else {
       carry = Fd[(int64_t)(l0 + 1) * nl + j];
-      carryB = planck(c1, lk, sp[0].T2, ek);
+      carryB = planck(c1, hcl, sp[0].iT2, ek);
     }
   }
   struct GroupA {
@@ -829,14 +833,14 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     A.F_st = P.stale;
     // contracted table: mmr = 1, and (0 + a) + b == a + b for its non-negative terms
     const double kap = (P.vlo * P.wl + P.vhi * P.wh) + sig;
-    const double dm = P.dm, Tnew = P.T;
+    const double dm = P.dm, iTnew = P.iT;
     load(g + 2, P);
     A.dtau = dm * kap;
     A.w0 = fm::div(sig, sig + kap);
     // each lane forms its step's new Planck value; the group gathers them and resolves
     // (B1, B2) of its steps in order (emit: B2 is new and becomes the next B1; absorb: B1 is
     // new and becomes the next B2; emit's top step keeps B2 = B1)
-    const double X = planck(c1, lk, Tnew, ek);
+    const double X = planck(c1, hcl, iTnew, ek);
     // the step before this lane's holds the lane before it in the group (quad_perm
     // [0,0,2,2] for Q = 2, [0,0,1,2] for Q = 4), the group's first step the carried value;
     // emit's top step keeps B2 = B1 (it is the last step, so no later step reads it)
@@ -1122,8 +1126,8 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
       const int top = (dir == kEmit && i == nL - 1) ? 1 : 0;
       f->layer = i;
       f->top = top;
-      f->T1 = T[i];
-      f->T2 = top ? T[i] : T[i + 1];
+      f->iT1 = 1.0 / T[i];
+      f->iT2 = top ? f->iT1 : 1.0 / T[i + 1];
       const double p2 = top ? u.p_top2 : P[i + 1];
       f->dm = (P[i] - p2) / u.g;
       int64_t off;
@@ -1143,8 +1147,8 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
       const int top = (dir == kEmit && i == nL - 1) ? 1 : 0;
       f->layer = i;
       f->top = top;
-      f->T1 = T[i];
-      f->T2 = top ? T[i] : T[i + 1];
+      f->iT1 = 1.0 / T[i];
+      f->iT2 = top ? f->iT1 : 1.0 / T[i + 1];
       const double p2 = top ? u.p_top2 : P[i + 1];
       f->dm = (P[i] - p2) / u.g;
     }
@@ -1172,8 +1176,8 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
     StepP sp;
     sp.layer = i;
     sp.top = (dir == kEmit && i == nL - 1) ? 1 : 0;
-    sp.T1 = T[i];
-    sp.T2 = sp.top ? T[i] : T[i + 1];                         // twostream.py:358-363
+    sp.iT1 = 1.0 / T[i];
+    sp.iT2 = sp.top ? sp.iT1 : 1.0 / T[i + 1];                         // twostream.py:358-363
     const double p2 = sp.top ? u.p_top2 : P[i + 1];
     sp.dm = (P[i] - p2) / u.g;
     sp.pad = 0;
@@ -1602,7 +1606,8 @@ __global__ void propagate_kernel(int64_t n, const double* c1, const double* lk,
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   double u, d;
-  const double B1 = planck(c1[j], lk[j], T1), B2 = planck(c1[j], lk[j], T2);
+  const double hcl = kHC / lk[j];   // as the sweeps' host-side constant
+  const double B1 = planck(c1[j], hcl, 1.0 / T1), B2 = planck(c1[j], hcl, 1.0 / T2);
   if (g0)
     two_stream_g(w0[j], g0[j], dtau[j], B1, B2, F1u[j], F2d[j], u, d);
   else

@@ -77,7 +77,7 @@ int frei_ctx_destroy(frei_ctx* ctx);
 /*
  * Grid and per-wavelength constants (frei/core.py:113-188, 48-55; twostream.py:46-67).
  *   c1[n_lam]     2 h c^2 / lam^5                (Planck prefactor, BB)
- *   lk[n_lam]     lam * k_B                      (BB exponent is h c / (lk * T))
+ *   lk[n_lam]     lam * k_B   (BB exponent h c / (lk T), formed as (h c / lk) * (1 / T))
  *   sigma[n_lam]  Rayleigh H2 + He, cm^2 g^-1    (opacity.py:173-200, 233)
  *   f_toa[n_lam]  stellar flux at TOA            (core.py:48-55)
  *   trapz_w[n_lam] per-point trapezoid weights of the GLOBAL grid (cm), sliced
