@@ -289,10 +289,11 @@ struct SweepArgs {
 
 // P2P exchange of the per-sweep bolometric partial sums over xGMI, no RCCL and no host in the
 // loop.  Every rank owns a mailbox in uncached device memory that every other
-// rank has mapped through an IPC handle; per sweep each rank's reduce kernel pushes its n sums
-// into slot [rank] of every mailbox, then a sequence flag per value; the update kernel polls
-// its own mailbox until every rank's flags carry the sweep's sequence number and sums the
-// ranks in rank order.  Two parity slots: a rank can run at most one sweep ahead of another
+// rank has mapped through an IPC handle; per sweep each rank pushes its n sums into slot
+// [rank] of every mailbox, then a sequence flag per value, and polls its own mailbox until
+// every rank's flags carry the sweep's sequence number, summing the ranks in rank order (the
+// fused update kernel does both, one workgroup per layer; with fused_update 0 the reduce
+// kernel pushes and the update kernel waits).  Two parity slots: a rank can run at most one sweep ahead of another
 // (its next update needs everyone's next sums), so slot seq & 1 is never overwritten while a
 // slower rank still reads it.
 struct P2PPush {

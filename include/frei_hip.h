@@ -180,9 +180,9 @@ int frei_comm_init(frei_ctx* ctx, int nranks, int rank, const void* id128);
  * mailbox in uncached device memory and exports its 64-byte IPC handle
  * (frei_comm_p2p_handle); after the handles are all-gathered out of band (rank order),
  * frei_comm_p2p_open maps every rank's mailbox and runs a bounded handshake.  Per sweep the
- * reduce kernel pushes this rank's n_layers*4 partial sums into every mailbox with a
- * sequence flag per value, and the update kernel waits for every rank's flags (a rank that
- * never publishes is reported as an error after FREI_P2P_TIMEOUT_S seconds, default 30).
+ * update kernel pushes this rank's n_layers*4 partial sums into every mailbox with a
+ * sequence flag per value and waits for every rank's flags (a rank that never publishes is
+ * reported as an error after FREI_P2P_TIMEOUT_S seconds, default 30).
  * Ranks may share one GPU (processes on the same device).
  */
 int frei_comm_p2p_handle(frei_ctx* ctx, int nranks, int rank, void* handle64);
