@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-per-species", action="store_true",
                     help="skip the per-species (no K3 contraction) measurement")
     ap.add_argument("--per-species-steps", type=int, default=6)
+    ap.add_argument("--no-chemistry", action="store_true",
+                    help="skip the T-dependent chemistry measurement (one GPU only)")
     ap.add_argument("--no-c5", action="store_true",
                     help="skip the batched-atmosphere (C5) measurement")
     ap.add_argument("--c5-lam", type=int, default=100_000)
@@ -421,6 +423,33 @@ def main():
                          f"iteration + final emit, {dt:.1f} s"}
     eng.close()
 
+    # ---- T-dependent chemistry (mmr tabulated on (T, p), re-interpolated on the device before
+    # every sweep; per-species sweep): the same fixed work, and the run to radiative equilibrium
+    chem = None
+    if d.world == 1 and not a.no_chemistry and not a.force_comm:
+        from frei_amd.engine import Engine
+        from frei_amd.workloads import c3_chemistry
+        ce = Engine(w["lam"], w["p"], tabs, mmr=c3_chemistry(w), device=d.local)
+        try:
+            cpath = ce.path()
+            ce.state_init(w["T0"])
+            el_c = timed_iterations(ce, d, 2, a.per_species_steps)
+            ce.run(w["T0"], n_timesteps=a.rad_eq_max, n_zero_crossings=2, convergence_dT=3.0,
+                   alpha=1.0, want_dtaus=False)
+            t4 = time.perf_counter()
+            cout = ce.run(w["T0"], n_timesteps=a.rad_eq_max, n_zero_crossings=2,
+                          convergence_dT=3.0, alpha=1.0, want_dtaus=False)
+            t5 = time.perf_counter()
+        finally:
+            ce.close()
+        chem = {"value": updates_per_step * a.per_species_steps / el_c, "unit": "updates/s",
+                "ms_per_step": el_c / a.per_species_steps * 1e3, "steps": a.per_species_steps,
+                "path": cpath,
+                "rad_eq": {"iterations": cout["n_iter"], "wall_s": t5 - t4,
+                           "iters_per_s": cout["n_iter"] / (t5 - t4)},
+                "note": "synthetic T-dependent mixing ratios (frei_amd.workloads.c3_chemistry) "
+                        "re-interpolated per layer before every sweep; per-species sweep (no K3)"}
+
     # PMC traffic / VALU of the same workload (separate rocprofv3 --pmc passes, committed)
     traffic, traffic_src, valu = None, None, None
     tpath = os.path.join(ROOT, "profiles", "traffic_sweep.json")
@@ -501,6 +530,7 @@ def main():
                                      "HBM peak because K3 hoists the species sum out of the "
                                      "loop"}},
             "per_species": per_species,
+            "chemistry": chem,
             "cpu_baseline": cpu,
             "k6_binning": binning,
             "c5_batched": c5,

@@ -59,6 +59,20 @@ def c3(n_layers=60, n_lam=500_000, n_T=16, T_ref=1500.0, species=None, seed=42):
                 mmr=np.array(rows))
 
 
+def c3_chemistry(w, n_T=14, n_p=9):
+    """A T-dependent chemistry table for the C3 species (frei_amd.ChemistryTable): mass
+    mixing ratios on (T, p) nodes around each species' median C3 value, half of the species
+    falling with T and half rising (a tanh around 1500 K, weak log-p slope).  Synthetic: the
+    reference's FastChem is third-party and absent."""
+    from .chemistry import ChemistryTable
+    cT = np.linspace(300.0, 4000.0, n_T)
+    cp = np.logspace(-7, 3, n_p)
+    x = np.tanh((cT[:, None] - 1500.0) / 400.0) + 0.05 * np.log10(cp)[None, :]
+    vals = {n: float(np.median(w["mmr"][s])) * 10 ** (0.5 * (-1) ** s * x)
+            for s, n in enumerate(w["names"])}
+    return ChemistryTable(vals, cT, cp)
+
+
 def bytes_per_update(n_species, write_dtau=False, live_only=False):
     """Algorithmic HBM bytes per (layer, wavelength) flux update:
     stale opposite-stream read 8 + two flux writes 16 + two T-bracket rows per species.

@@ -36,15 +36,10 @@ def _tables():
 
 
 def _chem(fa, w):
-    """T-dependent chemistry for the C3 species (mmr on (T, p) nodes around each species'
-    median mixing ratio: half the species fall with T, half rise), re-interpolated on the
-    device before every sweep; the sweep keeps the per-species sum."""
-    cT = np.linspace(300.0, 4000.0, 14)
-    cp = np.logspace(-7, 3, 9)
-    x = np.tanh((cT[:, None] - 1500.0) / 400.0) + 0.05 * np.log10(cp)[None, :]
-    vals = {n: float(np.median(w["mmr"][s])) * 10 ** (0.5 * (-1) ** s * x)
-            for s, n in enumerate(w["names"])}
-    return fa.ChemistryTable(vals, cT, cp)
+    """T-dependent chemistry for the C3 species (frei_amd.workloads.c3_chemistry), re-interpolated
+    on the device before every sweep; the sweep keeps the per-species sum."""
+    from frei_amd.workloads import c3_chemistry
+    return c3_chemistry(w)
 
 
 def _free_port():

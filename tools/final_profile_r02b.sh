@@ -12,7 +12,7 @@ cat $O/smoke.log
 MASTER_ADDR=127.0.0.1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline --no-binning > $O/rehearsal_n2.json 2> $O/rehearsal_n2.err
 cat $O/rehearsal_n2.json
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-B="python3 bench.py --steps 10 --warmup 1 --rad-eq-max 1 --no-cpu-baseline --no-binning --no-c5 --no-per-species"
+B="python3 bench.py --steps 10 --warmup 1 --rad-eq-max 1 --no-cpu-baseline --no-binning --no-c5 --no-per-species --no-chemistry"
 SQ="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 for mode in 1 0; do
   export FREI_PRECONTRACT=$mode
@@ -29,7 +29,7 @@ cp profiles/traffic_sweep*.json profiles/valu_sweep*.json $O/
 timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --no-cpu-baseline > $O/bench_under_rocprof.json 2> $O/bench_under_rocprof.err
 for n in 250000 125000 62500; do
-  timeout -k 10 120 python3 bench.py --n-lam $n --steps 20 --no-binning --no-cpu-baseline --no-c5 --no-per-species > $O/bench_n$n.json 2>/dev/null
+  timeout -k 10 120 python3 bench.py --n-lam $n --steps 20 --no-binning --no-cpu-baseline --no-c5 --no-per-species --no-chemistry > $O/bench_n$n.json 2>/dev/null
   timeout -k 10 120 python3 bench.py --n-lam $n --steps 20 --no-binning --no-cpu-baseline --no-c5 --no-per-species --force-comm > $O/bench_n${n}_p2p.json 2>/dev/null
 done
 timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/prof_n62500 -o run -- python3 bench.py --n-lam 62500 --steps 20 --rad-eq-max 1 --no-binning --no-cpu-baseline --no-c5 --no-per-species --force-comm > $O/bench_n62500_under_rocprof.json 2>/dev/null

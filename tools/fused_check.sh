@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method threa
   tests/test_gpu_fused_update.py tests/test_gpu_multirank.py tests/test_gpu_rccl.py \
   > $O/pytest.log 2>&1
 rc=$?; tail -15 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
-B="python3 bench.py --steps 20 --warmup 5 --rad-eq-max 1 --no-cpu-baseline --no-binning --no-c5 --no-per-species"
+B="python3 bench.py --steps 20 --warmup 5 --rad-eq-max 1 --no-cpu-baseline --no-binning --no-c5 --no-per-species --no-chemistry"
 for n in 500000 62500; do
   for f in 1 0; do
     FREI_FUSED_UPDATE=$f timeout -k 10 200 $B --n-lam $n --force-comm > $O/bench_${n}_f$f.json 2>/dev/null || exit $?

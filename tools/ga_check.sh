@@ -6,7 +6,7 @@ mkdir -p $O
 FREI_GROUP_AHEAD=4 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
   tests/test_gpu_parity.py -k "grouped" > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
-B="python3 bench.py --steps 30 --warmup 5 --rad-eq-max 1 --no-cpu-baseline --no-binning --no-c5 --no-per-species"
+B="python3 bench.py --steps 30 --warmup 5 --rad-eq-max 1 --no-cpu-baseline --no-binning --no-c5 --no-per-species --no-chemistry"
 for rep in 1 2; do
 for n in 47000 62500 94000; do
   for ga in 2 4; do

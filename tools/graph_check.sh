@@ -6,7 +6,7 @@ mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
   > $O/pytest.log 2>&1
 rc=$?; tail -5 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
-B="python3 bench.py --steps 40 --warmup 8 --rad-eq-max 1 --no-cpu-baseline --no-binning --no-c5 --no-per-species"
+B="python3 bench.py --steps 40 --warmup 8 --rad-eq-max 1 --no-cpu-baseline --no-binning --no-c5 --no-per-species --no-chemistry"
 for rep in 1 2; do
 for n in 500000 62500; do
   for g in 1 0; do

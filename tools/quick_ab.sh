@@ -7,7 +7,7 @@ ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 400 --timeout-method thread \
   > gpurun_out/$TAG/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/$TAG/pytest.log; ok $rc || exit $rc
-B="python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-binning --no-c5 --no-per-species"
+B="python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-binning --no-c5 --no-per-species --no-chemistry"
 for n in 500000 62500; do
   timeout -k 10 200 $B --n-lam $n > gpurun_out/$TAG/bench_$n.json 2>/dev/null || exit $?
   python3 -c "import json;d=json.load(open('gpurun_out/$TAG/bench_$n.json'));print($n, 'ms/step %.4f'%d['ms_per_step'], 'sweep %.4f'%d['roofline']['avg_launch_ms'], d['sweep_path'])"

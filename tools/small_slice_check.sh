@@ -7,7 +7,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
   tests/test_gpu_parity.py -k "grouped or contraction or c1" tests/test_gpu_fused_update.py \
   > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
-B="python3 bench.py --steps 30 --warmup 5 --rad-eq-max 1 --no-cpu-baseline --no-binning --no-c5 --no-per-species"
+B="python3 bench.py --steps 30 --warmup 5 --rad-eq-max 1 --no-cpu-baseline --no-binning --no-c5 --no-per-species --no-chemistry"
 for rep in 1 2; do
 for n in 62500 125000; do
   timeout -k 10 200 $B --n-lam $n > $O/bench_${n}_$rep.json 2>/dev/null || exit $?
