@@ -13,14 +13,22 @@
 //     albedos, 1/chi) is far from them, so the bare core below returns the same bits.
 //   * sqrt's denormal-range scaling (x < 2^-767) is likewise dropped: the sweep takes square
 //     roots of 1 - w0 style quantities in (2^-53, 2].
-// Every function keeps the exact operation sequence of the lowering it replaces (same
-// constants, same fma order), so results are identical wherever the dropped guards would not
-// fire; tools/mathcheck.hip checks that on the GPU over random and edge-case inputs.
+//   * division and sqrt refine the hardware estimate with one Newton-Raphson step fewer than
+//     the LLVM / ocml sequences (FREI_FM_DIV / FREI_FM_SQRT = 2): gfx950's v_rcp_f64 and
+//     v_rsq_f64 are good to ~2^-24 and one step brings the reciprocal to <= 11 ulp
+//     (tools/rcp_acc.hip), after which the quotient's residual correction (sqrt: the final
+//     Newton correction) still rounds correctly — 0 differences from the IEEE result in 2^28
+//     random operands per range (tools/mathcheck.hip).  Not a proof: a result within ~2^-45
+//     ulp of a rounding midpoint could come out one ulp off (probability ~2^-44 per call).
+//     -1.2 % sweep time at 500k, -3.9 % at 62.5k (profiles/r02_ab_short_div.txt).
+// Otherwise every function keeps the exact operation sequence of the lowering it replaces
+// (same constants, same fma order), so results are identical wherever the dropped guards
+// would not fire; tools/mathcheck.hip checks that on the GPU over random and edge-case inputs.
 #pragma once
 #include <hip/hip_runtime.h>
 
-// A/B switches (tools/build_variant.sh -DFREI_FM_...=0|1): 0 selects the plain ocml / IEEE
-// form.  FREI_FM_EXP is off: in the sweep the SGPR-held coefficients push the kernel past
+// A/B switches (tools/build_variant.sh -DFREI_FM_...=0|1|2): 0 selects the plain ocml / IEEE
+// form, 1 the full-length sequences without range guards, 2 (div, sqrt) one step fewer.  FREI_FM_EXP is off: in the sweep the SGPR-held coefficients push the kernel past
 // the SGPR file (18 spills through v_writelane/v_readlane), which measured 2% slower than the
 // VGPR moves it removes (profiles/r01_ab_fastmath.txt).  Division and sqrt are on (-6%).
 #ifndef FREI_FM_EXP
@@ -30,10 +38,10 @@
 #define FREI_FM_EXPM1 FREI_FM_EXP
 #endif
 #ifndef FREI_FM_DIV
-#define FREI_FM_DIV 1
+#define FREI_FM_DIV 2
 #endif
 #ifndef FREI_FM_SQRT
-#define FREI_FM_SQRT 1
+#define FREI_FM_SQRT 2
 #endif
 
 namespace frei {
@@ -212,8 +220,8 @@ __device__ __forceinline__ double rcp_nr(double b) {
   return __builtin_fma(r, e, r);
 }
 
-// a / b: LLVM's fp64 division core (rcp, two Newton-Raphson steps, quotient, one residual
-// correction) without the div_scale / div_fmas / div_fixup range guards.
+// a / b: LLVM's fp64 division core (rcp, two Newton-Raphson steps — one with FREI_FM_DIV 2 —,
+// quotient, one residual correction) without the div_scale / div_fmas / div_fixup guards.
 __device__ __forceinline__ double div(double a, double b) {
 #if !FREI_FM_DIV
   return a / b;
@@ -221,8 +229,10 @@ __device__ __forceinline__ double div(double a, double b) {
   double r = __builtin_amdgcn_rcp(b);
   double e = __builtin_fma(-b, r, 1.0);
   r = __builtin_fma(r, e, r);
+#if FREI_FM_DIV != 2
   e = __builtin_fma(-b, r, 1.0);
   r = __builtin_fma(r, e, r);
+#endif
   const double q = a * r;
   const double rem = __builtin_fma(-b, q, a);
   return __builtin_fma(rem, r, q);
@@ -237,8 +247,8 @@ __device__ __forceinline__ double div_big(double a, double b) {
   return q;
 }
 
-// sqrt(x): ocml's rsq + Newton-Raphson sequence without the x < 2^-767 rescaling; +-0 and
-// +inf pass through as in ocml.
+// sqrt(x): ocml's rsq + Newton-Raphson sequence (its last correction dropped with
+// FREI_FM_SQRT 2) without the x < 2^-767 rescaling; +-0 and +inf pass through as in ocml.
 __device__ __forceinline__ double sqrt(double x) {
 #if !FREI_FM_SQRT
   return ::sqrt(x);
@@ -251,8 +261,10 @@ __device__ __forceinline__ double sqrt(double x) {
   h = __builtin_fma(h, e, h);
   double d = __builtin_fma(-g, g, x);
   g = __builtin_fma(d, h, g);
+#if FREI_FM_SQRT != 2
   d = __builtin_fma(-g, g, x);
   g = __builtin_fma(d, h, g);
+#endif
   return __builtin_amdgcn_class(x, 0x260) ? x : g;   // +-0, +inf
 }
 
