@@ -10,6 +10,7 @@ between builds (MI355X guide §5.4 rule 24) and report median / min ms per sweep
 import ctypes
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -58,12 +59,15 @@ def main():
         eng.iterate(1)
         eng.synchronize()
         builds.append((name, lib, eng, []))
+    res_it = {}
     for r in range(rounds):
         for name, lib, eng, res in builds:
             N._lib = lib
             eng.timing(True)
+            t0 = time.perf_counter()
             eng.iterate(iters)
             eng.synchronize()
+            res_it.setdefault(name, []).append((time.perf_counter() - t0) * 1e3 / iters)
             ms, n = eng.timing_read()
             eng.timing(False)
             res.append(ms / n)
@@ -72,7 +76,8 @@ def main():
         med = float(np.median(res))
         print(f"{name:>14s}: sweep median {med:.4f} ms  min {min(res):.4f} ms  "
               f"{bpu * (w['p'].size - 1) * n_lam / (min(res) * 1e-3) / 1e12:.3f} TB/s algorithmic "
-              f"({n_lam} lambda, {S} species)")
+              f"({n_lam} lambda, {S} species); T-P iteration median "
+              f"{float(np.median(res_it[name])):.4f} ms (wall, {iters} per round)")
     for name, lib, eng, res in builds:   # close every context with its own library
         N._lib = lib
         eng.close()
