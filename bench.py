@@ -42,6 +42,8 @@ def parse():
                     help="max T-P iterations for the iterations-to-radiative-equilibrium run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-lam", type=int, default=50_000)
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
+                    help="threads of the all-cores CPU leg (1 = skip it)")
     ap.add_argument("--no-binning", action="store_true",
                     help="skip the K6 opacity-binning measurement (rank 0)")
     ap.add_argument("--binning-reps", type=int, default=5)
@@ -110,6 +112,38 @@ def cpu_baseline(w, n_sample, steps=1):
                         n_zero_crossings=10 ** 9, convergence_dT=-1.0, mmr=w["mmr"])
     dt = time.perf_counter() - t0
     updates = (2 * steps + 1) * (w["p"].size - 1) * n_sample   # incl. the final emit
+    return updates / dt, dt
+
+
+def cpu_baseline_threads(w, n_per_thread, threads, steps=1):
+    """The oracle λ-sharded over `threads` host threads (SURVEY.md §8(d)'s optional all-cores
+    variant): each thread runs the same path on its own disjoint wavelength sample of
+    `n_per_thread` (NumPy's ufuncs release the GIL on these array sizes).  Timing only — the
+    shards do not exchange their bolometric sums, so their temperatures are not the unsharded
+    run's — the same arithmetic per update as cpu_baseline.  Threads, not processes: this
+    process already holds a GPU context."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import frei_oracle as O
+    lam = w["lam"]
+    idx_all = np.linspace(0, lam.size - 1, n_per_thread * threads).round().astype(int)
+    jobs = []
+    for t in range(threads):
+        idx = idx_all[t::threads]
+        tabs = {n: O.Table(O.SeparableValues(w["base"][s][idx], w["fp"][s], w["fT"][s]),
+                           w["p"], w["T_nodes"]) for s, n in enumerate(w["names"])}
+        jobs.append((tabs, lam[idx], O.F_TOA(lam[idx])))
+
+    def one(job):
+        tabs, lam_s, Ft = job
+        O.emission_spectrum(tabs, w["T0"], w["p"], lam_s, Ft, 2478.6519476149147,
+                            4.0142926168559996e-24, 1, n_timesteps=steps,
+                            n_zero_crossings=10 ** 9, convergence_dT=-1.0, mmr=w["mmr"])
+
+    with ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(one, jobs))
+        dt = time.perf_counter() - t0
+    updates = (2 * steps + 1) * (w["p"].size - 1) * n_per_thread * threads
     return updates / dt, dt
 
 
@@ -421,6 +455,15 @@ def main():
                          f"{os.cpu_count()} host CPUs), {nL} layers x {min(a.cpu_lam, n_lam)} "
                          f"lambda (evenly strided sample of the same grid), {S} species, 1 T-P "
                          f"iteration + final emit, {dt:.1f} s"}
+        if a.cpu_threads > 1:
+            n_t = max(1, min(a.cpu_lam, n_lam) // 4)
+            rate_t, dt_t = cpu_baseline_threads(w, n_t, a.cpu_threads)
+            cpu["all_cores"] = {
+                "value": rate_t, "unit": "updates/s", "cores": a.cpu_threads,
+                "speedup_over_1_core": rate_t / rate,
+                "sample": f"the same oracle path lambda-sharded over {a.cpu_threads} threads "
+                          f"({n_t} lambda each, disjoint strided samples, no exchange of "
+                          f"bolometric sums between shards: timing only), {dt_t:.1f} s"}
     eng.close()
 
     # ---- T-dependent chemistry (mmr tabulated on (T, p), re-interpolated on the device before
