@@ -366,6 +366,22 @@ def main():
     path = eng.path()
     setup_ms = (time.perf_counter() - t_s) * 1e3
     setup_phases = eng.setup_timing()
+    if kind == "p2p" and d.world > 1:
+        # one untimed T-P iteration through the mailboxes: a peer whose sums never arrive
+        # fails every rank within FREI_P2P_TIMEOUT_S, and the run goes on over RCCL instead
+        err = None
+        try:
+            eng.state_init(w["T0"])
+            eng.iterate(1)
+            eng.synchronize()
+        except RuntimeError as e:
+            err = str(e)
+        if not d.all_ok(err is None):
+            eng.close()
+            comm_note = f"p2p exchange failed at run time ({err or 'on a peer rank'}); " \
+                        "fell back to RCCL"
+            kind = "rccl"
+            eng = build_engine(w, tabs, lo, hi, d, kind, a.force_comm)
 
     # ---- headline: timed fixed-work T-P iterations (no per-kernel events inside)
     eng.state_init(w["T0"])
