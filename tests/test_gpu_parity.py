@@ -648,3 +648,59 @@ def test_temperature_dependent_chemistry_matches_oracle(fa, case):
     m0 = np.array([chem_o(t, pb) for t, pb in zip(T0, p)])
     m1 = np.array([chem_o(t, pb) for t, pb in zip(out["final_T"], p)])
     assert np.max(np.abs(m1 - m0) / m0) > 1e-3
+
+
+@pytest.mark.parametrize("precontract", ["1", "0"])
+def test_high_albedo_lanes_match_oracle(fa, monkeypatch, precontract):
+    """Q9: omega_0 > 0.1 takes E(omega_0) (twostream.py:70-94) and the general step; short
+    wavelengths with weak line opacity put about half the lanes there, mixed inside most
+    64-lane waves, so both step forms run in one wave.  Every lane form (one, two and four
+    lanes per wavelength; the grouped forms take the contracted table only) against the
+    oracle, 3 T-P iterations, contracted and per-species."""
+    rng = np.random.default_rng(41)
+    lam, _, _ = O.wavelength_grid(0.3, 3, 2048)
+    nL = 20
+    p = O.pressure_grid(nL, -6, np.log10(200))
+    T0 = O.temperature_grid(p, 1600.0, 0.1, 0.1)
+    Tn = np.linspace(0.8 * T0.min(), 1.2 * T0.max(), 6)
+    names = ["1H2-16O", "12C-16O"]
+    mmr = O.mock_mmr(names, M_BAR)[:, None] * np.ones(nL)
+    tabs_o, tabs_f = {}, {}
+    for n in names:
+        base = 10 ** rng.uniform(-4, 0, lam.size)
+        fp, fT = (p / 1.0) ** 0.1, (Tn / 1000.0) ** 0.5
+        tabs_o[n] = O.Table(O.separable_table(base, fp, fT), p, Tn)
+        tabs_f[n] = fa.SeparableTable(base, fp, fT, p, Tn)
+    # the albedo the first sweep sees: a mix, and mixed within waves
+    k, sig = O.kappa(tabs_o, T0[5], p[5], lam, M_BAR, mmr=mmr[:, 5])
+    w0 = sig / (sig + k)
+    frac = (w0 > 0.1).mean()
+    mixed = np.mean([0 < (w0[i:i + 64] > 0.1).mean() < 1 for i in range(0, lam.size, 64)])
+    assert 0.2 < frac < 0.8 and mixed > 0.5, (frac, mixed)
+    cond = _cond((nL, lam.size))
+    osp, oT, oth, odt, ou, od, it = O.emission_spectrum(
+        tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1, n_timesteps=3,
+        n_zero_crossings=10 ** 6, convergence_dT=-1, mmr=mmr, err=cond)
+    floor = _floor(lambda: O.emission_spectrum(
+        tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1, n_timesteps=3,
+        n_zero_crossings=10 ** 6, convergence_dT=-1, mmr=mmr))
+    monkeypatch.setenv("FREI_PRECONTRACT", precontract)
+    for q in ((1, 2, 4) if precontract == "1" else (1,)):
+        monkeypatch.setenv("FREI_GROUP_Q", str(q))
+        eng = fa.Engine(lam, p, tabs_f, mmr=mmr)
+        try:
+            path = eng.path()
+            assert (path["paired"], path["quad"]) == (q == 2, q == 4)
+            assert path["contracted"] == (precontract == "1")
+            r = eng.run(T0, n_timesteps=3, n_zero_crossings=10 ** 6, convergence_dT=-1.0)
+            up, down = eng.get_fluxes()
+        finally:
+            eng.close()
+        what = f"high albedo Q{q} precontract {precontract}"
+        relT = rel(r["final_T"], oT)
+        assert relT < 1e-10, (what, relT)
+        delta = max(EPS, relT)
+        assert_flux_parity(r["spectrum"], osp, cond["up"][-1], delta, what + " spectrum")
+        assert_flux_parity(up, ou, cond["up"], delta, what + " F_up")
+        assert_flux_parity(down, od, cond["down"], delta, what + " F_down")
+        assert_grid_parity(r["spectrum"], osp, up, ou, down, od, what, floor)
