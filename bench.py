@@ -256,7 +256,10 @@ def c5_leg(a, d):
             "rad_eq": {"wall_s": rad, "atmospheres_per_s": A * d.world / rad,
                        "iterations_min": int(out["n_iter"].min()),
                        "iterations_max": int(out["n_iter"].max()),
-                       "max_iterations": a.rad_eq_max},
+                       "max_iterations": a.rad_eq_max,
+                       "converged_rank0": int((out["n_iter"] < a.rad_eq_max).sum()),
+                       "note": "iterations per atmosphere under the reference's convergence "
+                               "test; an atmosphere at max_iterations did not meet it"},
             "setup_s": setup_s,
             "note": "setup_s: table generation + metadata + K7 MFMA contraction, once"}
 

@@ -360,6 +360,10 @@ void launch_sweep_fast(int dir, int S, int depth, bool nan_check, bool shared,
 // Grouped-lane sweep (Q = 2 or 4 lanes per wavelength, 256/Q wavelengths per block):
 // contracted single table, step table in LDS; for slices with about one wave per SIMD.
 void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStream_t st);
+// producer/consumer sweep: NC consumer waves (64 NC wavelengths) per block, table rows PF
+// phases ahead
+void launch_sweep_pipe(int dir, int NC, int PF, const FastArgs& a, int nblocks, hipStream_t st);
+size_t pipe_lds_bytes(int NC, int M, int ns);
 void launch_nan_scan(const double* x, int64_t n, int* flag, hipStream_t st);
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
                    int force, hipStream_t st, int n_atm = 1, int64_t part_stride = 0,

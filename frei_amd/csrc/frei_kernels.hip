@@ -1003,6 +1003,284 @@ void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStrea
 }
 
 
+// ---------------------------------------------------------------- K1, producer/consumer form
+// Small slices again (the 8-GPU case), without the grouped form's replicated chain.  Only the
+// carried recurrence F = ic ((psi F_in - xi F_st) + X) is sequential over a wavelength's steps;
+// everything before it (opacity, dtau, albedo, Planck, E, the transmission, psi, xi, 1/chi and
+// the source terms — ~85 % of a step's instructions) is independent per (step, wavelength).
+// So per 64 wavelengths a block runs kPipeP = 3 producer waves and one consumer wave:
+//   phase ph: producer p computes the coefficients of the M consecutive steps
+//             ph G + p M ... (+ M - 1), G = 3 M, with the one-lane form's arithmetic (Planck
+//             reused inside its M steps, formed afresh at the first) into an LDS ring slot
+//             [ph & 1][G steps][psi, xi, ic, Xu, Xd][64 lanes] and writes dtau;
+//             the consumer runs the carried chain over phase ph - 1's G steps from the other
+//             slot (stale fluxes prefetched a phase ahead), stores the fluxes and stages the
+//             bolometric terms exactly as the one-lane sweep does;
+//   then one block barrier.
+// Four times the waves of the one-lane form per wavelength, each with a short dependent chain,
+// at ~1.1x its instructions per update (the extra Planck per M steps and the LDS hand-off).
+// Fluxes and dtaus are bit-identical to the one-lane form (same expressions, same order); with
+// NC = 4 consumers (256 wavelengths per block) the per-block bolometric partials are too (the
+// same lanes, staged tile and wave order), so T and every output match the one-lane sweep bit
+// for bit.  One contracted table (K3, mmr = 1); the step records come from the global step table
+// through scalar loads.
+constexpr int kPipeP = 3;    // producer waves per consumer wave
+constexpr int kPipeNV = 5;   // psi, xi, ic, Xu, Xd
+__host__ __device__ inline int64_t pipe_lds_doubles(int NC, int M, int ns) {
+  return (int64_t)NC * 2 * (kPipeP * M) * kPipeNV * 64 + (int64_t)NC * 2 * 4 * kStageRow +
+         (int64_t)NC * ns * 4;
+}
+
+template <int DIR, int NC, int M, int PF>
+__global__ __launch_bounds__(256 * NC) __attribute__((amdgpu_waves_per_eu(4)))
+void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
+                       double* __restrict__ Fd, double* __restrict__ part,
+                       double* __restrict__ dtaus) {
+  constexpr int G = kPipeP * M;   // steps per phase
+  static_assert(PF == 1 || PF == 2, "table rows loaded one or two phases ahead");
+  static_assert(G % 2 == 0, "phases hold whole step pairs (staged partial sums)");
+  {  // atmosphere of a batched launch (identity for one atmosphere)
+    const int m = blockIdx.y;
+    Fu += m * a.bs.flux;
+    Fd += m * a.bs.flux;
+    part += m * a.bs.part;
+    if (dtaus) dtaus += m * a.bs.flux;
+    ss += m * a.bs.steps;
+    a.tab[0] += m * a.bs.tab;
+    a.ftoa += m * a.bs.ftoa;
+    a.conv += m;
+  }
+  if (!a.force && *a.conv) return;
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sub = wv >> 2;    // 64-wavelength chunk of the block
+  // 0 .. 2: producer, 3: consumer (rotating the consumer across the chunks measured 3-5 %
+  // slower at 62.5k wavelengths)
+  const int role = wv & 3;
+  const int64_t nl = a.n_lam;
+  const int64_t j0 = (int64_t)blockIdx.x * (64 * NC) + sub * 64 + lane;
+  const bool act = j0 < nl;
+  const int64_t j = act ? j0 : nl - 1;
+  const int ns = a.n_steps;
+  const int nL = ns + 1;
+  const int nph = (ns + G - 1) / G;
+  double* ring = lds + (int64_t)sub * 2 * G * kPipeNV * 64;
+  double* tile = lds + (int64_t)NC * 2 * G * kPipeNV * 64;   // [sub][2][4][kStageRow]
+  double* red = tile + (int64_t)NC * 2 * 4 * kStageRow;      // [sub][ns][4]
+  auto rslot = [&](int ph, int s, int v) {
+    return ring + ((((ph & 1) * G + s) * kPipeNV + v) << 6) + lane;
+  };
+  if (role < kPipeP) {
+    // ---------------- producer
+    const int p = role;
+    const double c1 = a.c1[j], hcl = a.hcl[j], sig = a.sig[j];
+    const fm::Expm1Reg ek = fm::expm1_regs();
+    const double* __restrict__ tabj = a.tab[0] + j;
+    // a phase's table rows and step parameters, loaded PF phases ahead (two buffers when
+    // PF = 2: phases alternate between them, the loop below is unrolled by two)
+    struct Buf {
+      double vlo[M], vhi[M], wl[M], wh[M], dm[M], iTn[M], iT0;
+    };
+    auto load = [&](int ph, Buf& b) {
+      const int kb = min(ph * G + p * M, ns - 1);
+      b.iT0 = (DIR == kEmit) ? ss[kb].iT1 : ss[kb].iT2;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const int k = min(ph * G + p * M + i, ns - 1);
+        const FastStepS& st = ss[k];
+        const double* r = tabj + st.off;
+        b.vlo[i] = stream_load(r);
+        b.vhi[i] = stream_load(r + a.pitch);
+        b.wl[i] = st.wlo;
+        b.wh[i] = st.whi;
+        b.dm[i] = st.dm;
+        b.iTn[i] = (DIR == kEmit) ? st.iT2 : st.iT1;
+      }
+    };
+    auto produce = [&](int ph, Buf& b) {
+      if (ph >= nph) return;
+      const int kb = ph * G + p * M;
+      PreCoef pc[M];
+      StepCoef c[M];
+      // the Planck value the first step reuses in the one-lane form: emit B(T1), absorb
+      // B(T2) of step kb (the same inverse temperature as the previous step's new one)
+      double Bp = planck(c1, hcl, b.iT0, ek);
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const double kap = (b.vlo[i] * b.wl[i] + b.vhi[i] * b.wh[i]) + sig;
+        const double dtau = b.dm[i] * kap;
+        pc[i].w0 = fm::div(sig, sig + kap);
+        pc[i].dtau = dtau;
+        if (DIR == kEmit) {
+          const bool top = kb + i >= ns - 1;
+          pc[i].B1 = Bp;
+          pc[i].B2 = top ? Bp : planck(c1, hcl, b.iTn[i], ek);
+          Bp = pc[i].B2;
+        } else {
+          pc[i].B2 = Bp;
+          pc[i].B1 = planck(c1, hcl, b.iTn[i], ek);
+          Bp = pc[i].B1;
+        }
+      }
+      load(ph + PF, b);
+      bool e1 = true;
+#pragma unroll
+      for (int i = 0; i < M; ++i) e1 = e1 && !(pc[i].w0 > 0.1);
+      if (__all(e1)) {
+#pragma unroll
+        for (int i = 0; i < M; ++i) coef_e1(pc[i].w0, pc[i].dtau, pc[i].B1, pc[i].B2, c[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < M; ++i) coef_from(pc[i].w0, pc[i].dtau, pc[i].B1, pc[i].B2, c[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const int s = p * M + i;
+        *rslot(ph, s, 0) = c[i].psi;
+        *rslot(ph, s, 1) = c[i].xi;
+        *rslot(ph, s, 2) = c[i].ic;
+        *rslot(ph, s, 3) = c[i].Xu;
+        *rslot(ph, s, 4) = c[i].Xd;
+        if (dtaus && act && kb + i < ns) dtaus[(int64_t)(kb + i + 1) * nl + j] = c[i].dtau;
+      }
+    };
+    Buf b0, b1;
+    load(0, b0);
+    if constexpr (PF == 2) {
+      load(1, b1);
+      for (int ph = 0; ph <= nph; ph += 2) {   // nph + 1 barriers, like the consumer's
+        produce(ph, b0);
+        __syncthreads();
+        if (ph + 1 <= nph) {
+          produce(ph + 1, b1);
+          __syncthreads();
+        }
+      }
+    } else {
+      for (int ph = 0; ph <= nph; ++ph) {
+        produce(ph, b0);
+        __syncthreads();
+      }
+    }
+  } else {
+    // ---------------- consumer
+    const double wt = act ? a.wtr[j] : 0.0;
+    double carry = (DIR == kEmit) ? Fu[(int64_t)step_layer(DIR, 0, nL) * nl + j]
+                                  : Fd[(int64_t)(step_layer(DIR, 0, nL) + 1) * nl + j];
+    double stn[G];   // stale opposite-stream fluxes of the next phase
+    auto load_stale = [&](int ph) {
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int k = min(ph * G + i, ns - 1);
+        const int layer = step_layer(DIR, k, nL);
+        const double* src = (DIR == kEmit)
+                                ? (k == ns - 1 ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
+                                : Fu + (int64_t)layer * nl;
+        stn[i] = src[j];
+      }
+    };
+    load_stale(0);
+    double* t0 = tile + (int64_t)sub * 2 * 4 * kStageRow;
+    for (int ph = 0; ph <= nph; ++ph) {
+      if (ph >= 1) {
+        const int q = ph - 1;   // phase consumed now
+        double stc[G];
+#pragma unroll
+        for (int i = 0; i < G; ++i) stc[i] = stn[i];
+        load_stale(ph);
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+          const int k = q * G + i;
+          if (k < ns) {
+            const double psi = *rslot(q, i, 0), xi = *rslot(q, i, 1), ic = *rslot(q, i, 2);
+            const double Xu = *rslot(q, i, 3), Xd = *rslot(q, i, 4);
+            double F1u, F2d;
+            if (DIR == kEmit) { F1u = carry; F2d = stc[i]; } else { F2d = carry; F1u = stc[i]; }
+            const double F2u = ic * ((psi * F1u - xi * F2d) + Xu);
+            const double F1d = ic * ((psi * F2d - xi * F1u) + Xd);
+            const int layer = step_layer(DIR, k, nL);
+            const bool top = DIR == kEmit && k == ns - 1;
+            if (act) {
+              const bool st_up = (DIR == kEmit) ? !top : (!a.live_only || layer == 0);
+              const bool st_dn = (DIR == kAbsorb) || !a.live_only || top;
+              if (st_up) Fu[(int64_t)(layer + 1) * nl + j] = F2u;
+              if (st_dn) Fd[(int64_t)layer * nl + j] = F1d;
+            }
+            double* t = t0 + ((k & 1) * 4) * kStageRow + lane;
+            t[0] = wt * F2u;
+            t[kStageRow] = wt * F2d;
+            t[2 * kStageRow] = wt * F1u;
+            t[3 * kStageRow] = wt * F1d;
+            carry = (DIR == kEmit) ? F2u : F1d;
+          }
+          if (i & 1) {   // the pair's 8 (step, quantity) sums: the one-lane staged reduction
+            __builtin_amdgcn_wave_barrier();
+            const int o = lane >> 3;
+            const double* t = t0 + ((o >> 2) * 4 + (o & 3)) * kStageRow + (lane & 7);
+            double y = t[0];
+#pragma unroll
+            for (int r = 1; r < 8; ++r) y += t[8 * r];
+            y += dpp_bcast<0xB1>(y);    // quad_perm [1,0,3,2]
+            y += dpp_bcast<0x4E>(y);    // quad_perm [2,3,0,1]
+            y += dpp_bcast<0x141>(y);   // row_half_mirror
+            const int ks = k - 1 + (o >> 2);
+            if ((lane & 7) == 0 && ks < ns) red[((int64_t)sub * ns + ks) * 4 + (o & 3)] = y;
+            __builtin_amdgcn_wave_barrier();
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < ns * 4; idx += 256 * NC) {
+    double s = red[idx];
+    for (int w = 1; w < NC; ++w) s += red[(int64_t)w * ns * 4 + idx];
+    part[(int64_t)idx * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+template <int DIR, int NC, int M, int PF>
+static void launch_pipe_t(const FastArgs& a, int nblocks, hipStream_t st) {
+  const size_t shm = (size_t)pipe_lds_doubles(NC, M, a.n_steps) * sizeof(double);
+  static bool attr = false;   // dynamic LDS above 64 KiB needs the opt-in once per kernel
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_pipe_kernel<DIR, NC, M, PF>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    attr = true;
+  }
+  hipLaunchKernelGGL((sweep_pipe_kernel<DIR, NC, M, PF>),
+                     dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1), dim3(256 * NC), shm, st, a,
+                     a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+}
+
+template <int NC, int PF>
+static void launch_pipe_nc(int dir, const FastArgs& a, int nblocks, hipStream_t st) {
+  if (dir == kEmit) launch_pipe_t<kEmit, NC, 2, PF>(a, nblocks, st);
+  else launch_pipe_t<kAbsorb, NC, 2, PF>(a, nblocks, st);
+}
+
+// NC consumers (64 NC wavelengths) per block, M = 2 steps per producer and phase (M = 4 needs
+// more than the 128 VGPRs of 4 waves per SIMD and spills), table rows PF phases ahead.
+void launch_sweep_pipe(int dir, int NC, int PF, const FastArgs& a, int nblocks,
+                       hipStream_t st) {
+  if (PF == 2) {
+    if (NC == 4) launch_pipe_nc<4, 2>(dir, a, nblocks, st);
+    else if (NC == 2) launch_pipe_nc<2, 2>(dir, a, nblocks, st);
+    else launch_pipe_nc<1, 2>(dir, a, nblocks, st);
+  } else {
+    if (NC == 4) launch_pipe_nc<4, 1>(dir, a, nblocks, st);
+    else if (NC == 2) launch_pipe_nc<2, 1>(dir, a, nblocks, st);
+    else launch_pipe_nc<1, 1>(dir, a, nblocks, st);
+  }
+}
+
+size_t pipe_lds_bytes(int NC, int M, int ns) {
+  return (size_t)pipe_lds_doubles(NC, M, ns) * sizeof(double);
+}
+
 // ---------------------------------------------------------------- P2P exchange
 // System-scope stores of a value and then its flag into every rank's mailbox (P2PPush): the
 // release fence orders the value stores before the flag stores for any observer; the

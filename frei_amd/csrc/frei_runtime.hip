@@ -187,10 +187,19 @@ struct frei_ctx {
   int pair_max_blocks = 420;            // FREI_PAIR_MAX_BLOCKS (<= 107k lambda per GPU)
   int quad_max_blocks = 208;            // FREI_QUAD_MAX_BLOCKS (<= 53k lambda per GPU)
   int group_q = 0;                      // FREI_GROUP_Q forces 1, 2 or 4 lanes per wavelength
+  int pipe_nc = -1;                     // FREI_PIPE: producer/consumer sweep, 1/2/4 consumers per
+                                        // block, 0 off, -1 by slice size (pipe_*_blocks)
+  int pipe_min_blocks = 208;            // FREI_PIPE_MIN_BLOCKS / _MAX_BLOCKS: 256-wavelength
+  int pipe_max_blocks = -1;             // blocks per GPU where the auto choice takes NC = 4
+                                        // (-1: the CU count, one 16-wave block per CU)
+  int n_cu = 256;                       // hipDeviceProp multiProcessorCount
+  int pipe_m = 2;                       // steps per producer and phase
+  int pipe_pf = 1;                      // FREI_PIPE_PF: phases the producers load ahead (1, 2)
   int red_rows = 1;                     // FREI_RED_ROWS=0: full wave sums per step
   int red_stage = 1;                    // FREI_RED_STAGE=0: no staged sums (one-lane sweep)
   int depth4_max_blocks = 0;            // FREI_DEPTH4_MAX_BLOCKS (4 steps in flight: off, measured no faster)
   size_t lds_per_block = 64 * 1024;     // hipDeviceProp sharedMemPerBlock
+  size_t lds_optin = 64 * 1024;         // with the dynamic-LDS opt-in (gfx950: 160 KiB)
   bool ftoa_per_atm = false;            // batched: one F_TOA per atmosphere (frei_set_ftoa_batch)
   double setup_ms[5] = {0, 0, 0, 0, 0};  // last metadata build, by phase (frei_setup_timing)
   // T-dependent chemistry (frei_set_chemistry): mmr tables on (T, p) nodes
@@ -445,6 +454,21 @@ int group_lanes(frei_ctx* c) {
   return 1;
 }
 
+// Consumers per block of the producer/consumer sweep (0: not used).  Contracted table and the
+// FastStepS records (the LDS-step-table path); the block's LDS must fit the device.
+int pipe_consumers(frei_ctx* c) {
+  if (!(c->fast && c->eff && c->shared) || c->pipe_nc == 0) return 0;
+  int nc = c->pipe_nc;
+  if (nc < 0) {   // by slice size: one 256-wavelength block per CU or fewer
+    const int64_t blocks = (int64_t)c->nblocks * c->n_atm;
+    const int64_t mx = c->pipe_max_blocks < 0 ? c->n_cu : c->pipe_max_blocks;
+    if (blocks <= c->pipe_min_blocks || blocks > mx) return 0;
+    nc = 4;
+  }
+  if (pipe_lds_bytes(nc, c->pipe_m, c->nL - 1) > c->lds_optin) return 0;
+  return nc;
+}
+
 SetupArgs setup_args(frei_ctx* c) {
   SetupArgs u{};
   u.n_layers = c->nL;
@@ -588,12 +612,17 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
                 (size_t)ns * sizeof(FastStepS) <= 48 * 1024)
       f.red_rows = 2;
     if (Q > 1) nb_run = (int)((c->nlam + kBlock / Q - 1) / (kBlock / Q));
+    const int NC = pipe_consumers(c);
+    if (NC > 0) nb_run = (int)((c->nlam + 64 * NC - 1) / (64 * NC));
     if (c->keys) {
       uint64_t h = arg_hash(1469598103934665603ull, f);
-      const int cfg[6] = {o.dir, Q, S_run, depth, (nan_check && !c->eff) ? 1 : 0, c->shared};
+      const int cfg[8] = {o.dir, Q, S_run, depth, (nan_check && !c->eff) ? 1 : 0, c->shared,
+                          NC, c->pipe_pf};
       c->keys->push_back(arg_hash(h, cfg));
     }
     if (c->dry) {
+    } else if (NC > 0) {
+      launch_sweep_pipe(o.dir, NC, c->pipe_pf, f, nb_run, c->stream);
     } else if (Q > 1) {
       launch_sweep_group(o.dir, Q, f, nb_run, c->stream);
     } else {
@@ -769,7 +798,8 @@ bool ready(frei_ctx* c) { return c && c->grid_set; }
 const char* const kOptionNames[] = {"prefetch_depth", "shared", "shared_max_blocks",
                                     "precontract", "depth4_max_blocks", "pair_max_blocks",
                                     "quad_max_blocks", "red_rows", "red_stage", "group_q",
-                                    "fused_update", "graph", nullptr};
+                                    "fused_update", "graph", "pipe", "pipe_pf", "pipe_min_blocks",
+                                    "pipe_max_blocks", nullptr};
 int set_option(frei_ctx* c, const std::string& k, int v) {
   if (k == "prefetch_depth") c->prefetch_depth = v;
   else if (k == "shared") c->shared_mode = v < 0 ? -1 : (v ? 1 : 0);
@@ -783,6 +813,10 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "group_q") c->group_q = (v == 1 || v == 2 || v == 4) ? v : 0;
   else if (k == "fused_update") c->fused_update = v != 0;
   else if (k == "graph") c->use_graph = v != 0;
+  else if (k == "pipe") c->pipe_nc = (v == 1 || v == 2 || v == 4 || v == -1) ? v : 0;
+  else if (k == "pipe_min_blocks") c->pipe_min_blocks = v;
+  else if (k == "pipe_max_blocks") c->pipe_max_blocks = v;
+  else if (k == "pipe_pf") c->pipe_pf = v == 1 ? 1 : 2;
   else return fail("unknown option '" + k + "'");
   c->meta_dirty = true;
   return 0;
@@ -845,8 +879,11 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
   if ((rc = set_device(c))) return bail(rc);
   {
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.sharedMemPerBlock > 0)
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.sharedMemPerBlock > 0) {
       c->lds_per_block = prop.sharedMemPerBlock;
+      c->lds_optin = std::max(c->lds_per_block, (size_t)prop.sharedMemPerBlockOptin);
+      if (prop.multiProcessorCount > 0) c->n_cu = prop.multiProcessorCount;
+    }
   }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail("hipStreamCreate failed"));
@@ -1766,8 +1803,10 @@ int frei_ctx_path(frei_ctx* c, int* flags) {
   int nan = 0;
   for (const auto& q : c->sp) nan = nan || q.has_nan;
   const int Q = group_lanes(c);
+  const int NC = pipe_consumers(c);
   *flags = (c->fast ? 1 : 0) | (c->fast && c->shared ? 2 : 0) | (c->eff ? 4 : 0) |
-           (nan ? 8 : 0) | (Q == 2 ? 16 : 0) | (Q == 4 ? 32 : 0);
+           (nan ? 8 : 0) | (NC == 0 && Q == 2 ? 16 : 0) | (NC == 0 && Q == 4 ? 32 : 0) |
+           (NC << 6);
   return 0;
 }
 

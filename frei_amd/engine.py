@@ -291,7 +291,8 @@ class Engine:
         N.check(N.lib().frei_ctx_path(self._ctx, ctypes.byref(f)))
         v = f.value
         return dict(fast=bool(v & 1), lds_steps=bool(v & 2), contracted=bool(v & 4),
-                    nan=bool(v & 8), paired=bool(v & 16), quad=bool(v & 32))
+                    nan=bool(v & 8), paired=bool(v & 16), quad=bool(v & 32),
+                    pipe=(v >> 6) & 7)
 
     def set_option(self, name, value):
         """Tuning knob of include/frei_hip.h frei_set_option (e.g. "precontract", 0)."""

@@ -215,7 +215,8 @@ int frei_contribution(frei_ctx* ctx, const double* dtaus, const double* nu,
  * bit 0 fast path (on-node pressures, >= 2 T nodes, S <= 8), bit 1 step table staged in
  * LDS (shared brackets, small slices), bit 2 species-contracted table (K3), bit 3 tables
  * hold NaN (per-species nansum variant), bit 4 / bit 5 grouped-lane sweep with two / four
- * lanes per wavelength (small slices). */
+ * lanes per wavelength (small slices), bits 6-8: consumer waves per block of the
+ * producer/consumer sweep (1, 2 or 4; 0 = not used). */
 int frei_ctx_path(frei_ctx* ctx, int* flags);
 
 /* Tuning knobs (also FREI_<NAME> in the environment at context creation): "precontract"

@@ -5,6 +5,8 @@ checks are size-independent properties of the path:
 - determinism: two runs give bitwise identical temperatures, spectra and dtaus;
 - the grouped-lane sweep (2 lanes per wavelength, forced) against the one-lane sweep the
   full slice uses: temperatures within 1e-12 (only the bolometric summation tree differs);
+- the producer/consumer sweep (four consumers per block, forced at this size) against the
+  one-lane sweep: bitwise identical temperatures, spectra and dtaus;
 - the species contraction (K3) against the per-species sum in the sweep: within the
   parity tolerance (the species sum is reordered);
 - physical sanity: finite, positive fluxes and a spectrum that responds to T.
@@ -40,6 +42,7 @@ def test_full_size_properties(monkeypatch):
     runs = {}
     variants = (("default", {}), ("again", {}),
                 ("pair", {"FREI_GROUP_Q": "2", "FREI_SHARED_MAX_BLOCKS": "100000"}),
+                ("pipe", {"FREI_PIPE": "4", "FREI_SHARED_MAX_BLOCKS": "100000"}),
                 ("per_species", {"FREI_PRECONTRACT": "0"}))
     for name, env in variants:
         eng, w = _engine(monkeypatch, env)
@@ -47,6 +50,8 @@ def test_full_size_properties(monkeypatch):
             path = eng.path()
             if name == "pair":
                 assert path["paired"]
+            if name == "pipe":
+                assert path["pipe"] == 4
             if name == "per_species":
                 assert not path["contracted"]
             else:
@@ -60,6 +65,8 @@ def test_full_size_properties(monkeypatch):
     assert np.array_equal(a["dtaus"], b["dtaus"])
     assert np.isfinite(a["spectrum"]).all() and (a["spectrum"] > 0).all()
     assert np.isfinite(a["dtaus"]).all()
+    for k in ("final_T", "spectrum", "dtaus"):
+        assert np.array_equal(runs["pipe"][k], a[k]), k
     assert rel(runs["pair"]["final_T"], a["final_T"]) < 1e-12
     assert rel(runs["pair"]["spectrum"], a["spectrum"]) < 1e-9
     assert rel(runs["per_species"]["final_T"], a["final_T"]) < 1e-10

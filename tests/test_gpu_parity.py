@@ -543,6 +543,64 @@ def test_grouped_lane_sweep_matches_one_lane_form(fa, monkeypatch, n_layers, red
         assert row_normwise(out[q]["run"]["spectrum"], out[1]["run"]["spectrum"]) < 1e-9
 
 
+@pytest.mark.parametrize("n_layers", [34, 37, 60])   # 33 / 36 / 59 steps: partial phases
+def test_pipe_sweep_matches_one_lane_form(fa, monkeypatch, n_layers):
+    """The producer/consumer sweep (three producer waves form the step coefficients into an LDS
+    ring, one consumer wave runs the carried chain) uses the one-lane expressions in the same
+    order: fluxes and dtaus are bit-identical for 1, 2 and 4 consumers per block; with 4 (256
+    wavelengths per block, the one-lane block) the bolometric partials are too, so a T-P run
+    gives bit-identical temperatures and spectra; with 1 or 2 only the block-sum tree differs."""
+    rng = np.random.default_rng(17)
+    lam, _, _ = O.wavelength_grid(0.5, 10, 5000)   # 5000: a ragged last block for every form
+    p = O.pressure_grid(n_layers, -6, np.log10(200))
+    T0 = O.temperature_grid(p, 1600.0, 0.1, 0.1)
+    Tn = np.linspace(0.8 * T0.min(), 1.2 * T0.max(), 9)
+    names = ["1H2-16O", "12C-16O", "Na"]
+    tabs = {n: fa.SeparableTable(10 ** rng.uniform(-4, 2, lam.size), (p / 1.0) ** 0.1,
+                                 (Tn / 1000.0) ** 0.5, p, Tn) for n in names}
+    mmr = O.mock_mmr(names, M_BAR)[:, None] * np.ones(n_layers)
+    monkeypatch.setenv("FREI_GROUP_Q", "1")
+    out = {}
+    for nc in (0, 1, 2, 4):
+        monkeypatch.setenv("FREI_PIPE", str(nc))
+        eng = fa.Engine(lam, p, tabs, mmr=mmr)
+        try:
+            path = eng.path()
+            assert path["contracted"] and path["pipe"] == nc, path
+            r = {}
+            for d in (0, 1):    # emit then absorb from the same initial state
+                eng.set_temperatures(T0)
+                eng.set_fluxes(np.full((n_layers, lam.size), 1e9),
+                               np.full((n_layers, lam.size), 2e8))
+                r[d] = eng.sweep(d, alpha=1.0) + eng.get_fluxes()
+            r["run"] = eng.run(T0, n_timesteps=4, n_zero_crossings=10 ** 6,
+                               convergence_dT=-1.0)
+            r["fl"] = eng.get_fluxes()
+            out[nc] = r
+        finally:
+            eng.close()
+    for nc in (1, 2, 4):
+        for d in (0, 1):
+            dT_p, bol_p, dt_p, up_p, dn_p = out[nc][d]
+            dT_o, bol_o, dt_o, up_o, dn_o = out[0][d]
+            assert np.array_equal(up_p, up_o) and np.array_equal(dn_p, dn_o), f"NC{nc} dir {d}"
+            assert np.array_equal(dt_p, dt_o), f"NC{nc} dir {d} dtaus"
+            if nc == 4:
+                assert np.array_equal(bol_p, bol_o) and np.array_equal(dT_p, dT_o)
+            else:
+                assert row_normwise(bol_p, bol_o) < 1e-12
+                assert np.all(np.abs(dT_p - dT_o) <= 1e-10 * np.abs(dT_o) + 1e-300)
+        ro, rp = out[0]["run"], out[nc]["run"]
+        if nc == 4:
+            assert np.array_equal(rp["final_T"], ro["final_T"])
+            assert np.array_equal(rp["spectrum"], ro["spectrum"])
+            assert all(np.array_equal(a, b) for a, b in zip(out[nc]["fl"], out[0]["fl"]))
+            assert np.array_equal(rp["dtaus"], ro["dtaus"])
+        else:
+            assert rel(rp["final_T"], ro["final_T"]) < 1e-12
+            assert row_normwise(rp["spectrum"], ro["spectrum"]) < 1e-9
+
+
 def test_shims_reuse_device_context_and_vector_kappa(fa, golden):
     """emit/absorb/kappa keep their device context (uploaded tables) between calls with the
     same opacity dict: repeated calls hit the cache and give bitwise-identical results; kappa
@@ -685,18 +743,20 @@ def test_high_albedo_lanes_match_oracle(fa, monkeypatch, precontract):
         tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1, n_timesteps=3,
         n_zero_crossings=10 ** 6, convergence_dT=-1, mmr=mmr))
     monkeypatch.setenv("FREI_PRECONTRACT", precontract)
-    for q in ((1, 2, 4) if precontract == "1" else (1,)):
+    forms = [(1, 0), (2, 0), (4, 0), (1, 1), (1, 2), (1, 4)] if precontract == "1" else [(1, 0)]
+    for q, nc in forms:   # lanes per wavelength, producer/consumer sweep's consumers per block
         monkeypatch.setenv("FREI_GROUP_Q", str(q))
+        monkeypatch.setenv("FREI_PIPE", str(nc))
         eng = fa.Engine(lam, p, tabs_f, mmr=mmr)
         try:
             path = eng.path()
-            assert (path["paired"], path["quad"]) == (q == 2, q == 4)
+            assert (path["paired"], path["quad"], path["pipe"]) == (q == 2, q == 4, nc)
             assert path["contracted"] == (precontract == "1")
             r = eng.run(T0, n_timesteps=3, n_zero_crossings=10 ** 6, convergence_dT=-1.0)
             up, down = eng.get_fluxes()
         finally:
             eng.close()
-        what = f"high albedo Q{q} precontract {precontract}"
+        what = f"high albedo Q{q} pipe {nc} precontract {precontract}"
         relT = rel(r["final_T"], oT)
         assert relT < 1e-10, (what, relT)
         delta = max(EPS, relT)
