@@ -331,6 +331,21 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
 #ifndef FREI_NT
 #define FREI_NT 0
 #endif
+// Flux-row stores of the sweeps.  FREI_WT_STORE=1 (A/B): system-scope relaxed stores, which
+// gfx950 writes through the L2, so the sweep leaves no dirty flux lines for the end-of-kernel
+// L2 writeback.
+#ifndef FREI_WT_STORE
+#define FREI_WT_STORE 0
+#endif
+__device__ __forceinline__ void flux_store(double* p, double v) {
+#if FREI_WT_STORE
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  *p = v;
+#endif
+}
+
 __device__ __forceinline__ double stream_load(const double* p) {
 #if FREI_NT
   return __builtin_nontemporal_load(p);
@@ -628,8 +643,8 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       // are rewritten by absorb before any read, absorb's F_up rows >= 2 by the next emit).
       const bool st_up = (DIR == kEmit) ? !c.top : (!a.live_only || i == 0);
       const bool st_dn = (DIR == kAbsorb) || !a.live_only || c.top;
-      if (st_up) Fu[(int64_t)(i + 1) * nl + j] = F2u;
-      if (st_dn) Fd[(int64_t)i * nl + j] = F1d;
+      if (st_up) flux_store(Fu + (int64_t)(i + 1) * nl + j, F2u);
+      if (st_dn) flux_store(Fd + (int64_t)i * nl + j, F1d);
       if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = c.dtau;
     }
     if (PD == 2 && a.red_rows == 2) {   // staged: reduced per pair of steps (stage_reduce)
@@ -903,8 +918,8 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
       const bool last = k == ns - 1;
       const bool st_up = (DIR == kEmit) ? !last : (!a.live_only || last);
       const bool st_dn = (DIR == kAbsorb) || !a.live_only || last;
-      if (st_up) *pu = F2u;
-      if (st_dn) *pd = F1d;
+      if (st_up) flux_store(pu, F2u);
+      if (st_dn) flux_store(pd, F1d);
       if (dtaus) *pt = c.dtau;
     }
     pu += rstep;
@@ -1205,8 +1220,8 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
             if (act) {
               const bool st_up = (DIR == kEmit) ? !top : (!a.live_only || layer == 0);
               const bool st_dn = (DIR == kAbsorb) || !a.live_only || top;
-              if (st_up) Fu[(int64_t)(layer + 1) * nl + j] = F2u;
-              if (st_dn) Fd[(int64_t)layer * nl + j] = F1d;
+              if (st_up) flux_store(Fu + (int64_t)(layer + 1) * nl + j, F2u);
+              if (st_dn) flux_store(Fd + (int64_t)layer * nl + j, F1d);
             }
             double* t = t0 + ((k & 1) * 4) * kStageRow + lane;
             t[0] = wt * F2u;
