@@ -1260,11 +1260,13 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
 template <int DIR, int NC, int M, int PF>
 static void launch_pipe_t(const FastArgs& a, int nblocks, hipStream_t st) {
   const size_t shm = (size_t)pipe_lds_doubles(NC, M, a.n_steps) * sizeof(double);
-  static bool attr = false;   // dynamic LDS above 64 KiB needs the opt-in once per kernel
-  if (!attr) {
+  // dynamic LDS above 64 KiB needs the kernel's opt-in, raised whenever a launch needs more
+  // (deeper atmospheres: the partial-sum rows grow with the step count)
+  static size_t attr = 0;
+  if (shm > attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_pipe_kernel<DIR, NC, M, PF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    attr = true;
+    attr = shm;
   }
   hipLaunchKernelGGL((sweep_pipe_kernel<DIR, NC, M, PF>),
                      dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1), dim3(256 * NC), shm, st, a,
