@@ -245,6 +245,20 @@ __device__ __forceinline__ double wave_sum4(double q0, double q1, double q2, dou
   return group_sum4<1>(q0, q1, q2, q3, lane);
 }
 
+// The xor-32, 16, ..., 1 butterfly (acc += shfl_xor(acc, o)) on the VALU: permlane32 / 16 swaps
+// for the half and row levels, DPP for the in-row ones.  Every level pairs the same lanes and
+// adds the same two values (addition commutes), so the result is bit-identical to the shfl form
+// without its LDS round trip per level.  Whole wave active.
+__device__ __forceinline__ double butterfly_sum(double v, int lane) {
+  v = rows_sum32(v);
+  v = rows_sum16(v);
+  v += lane_xor<8>(v, lane);
+  v += lane_xor<4>(v, lane);
+  v += lane_xor<2>(v, lane);
+  v += lane_xor<1>(v, lane);
+  return v;
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1372,7 +1386,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
   double acc = 0.0;
   for (int b = threadIdx.x; b < nblocks; b += 256) acc += p[b];
   // fixed-order butterfly inside each wave, then the 4 wave sums in order: deterministic
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  acc = butterfly_sum(acc, threadIdx.x & 63);   // = the xor-32 ... 1 shfl butterfly
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1785,7 +1799,7 @@ __global__ __launch_bounds__(256) void update_fused_kernel(UpdateArgs a) {
     for (int b = tid; b < a.nblocks; b += 256)
       for (int j = 0; j < 8; ++j) acc[j] += pj[j][b];
     for (int j = 0; j < 8; ++j)
-      for (int o = 32; o > 0; o >>= 1) acc[j] += __shfl_xor(acc[j], o, 64);
+      acc[j] = butterfly_sum(acc[j], tid & 63);   // = the xor-32 ... 1 shfl butterfly
     if ((tid & 63) == 0)
       for (int j = 0; j < 8; ++j) wsum[tid >> 6][j] = acc[j];
   }
