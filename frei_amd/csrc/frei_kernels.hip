@@ -1372,7 +1372,17 @@ void launch_p2p_handshake(const P2PPush& push, const P2PWait& wait, hipStream_t 
 }
 
 // ---------------------------------------------------------------- partial sums
-__global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ part,
+// Threads of the partial-sum stage (reduce_kernel and the fused update): each thread adds every
+// kRedThreads-th block column, then the wave butterflies and the wave sums in wave order — the
+// same fixed tree in both kernels (bit-identical).  1024 threads (four times the loads in
+// flight) measured no faster at 62.5k or 500k (profiles/r02_ab_red_threads.txt).
+#ifndef FREI_RED_THREADS
+#define FREI_RED_THREADS 256
+#endif
+constexpr int kRedThreads = FREI_RED_THREADS;
+constexpr int kRedWaves = kRedThreads / 64;
+
+__global__ __launch_bounds__(kRedThreads) void reduce_kernel(const double* __restrict__ part,
                                                      int nblocks, double* __restrict__ Fb,
                                                      const int* conv, int force,
                                                      int64_t part_stride, int64_t fb_stride,
@@ -1381,16 +1391,17 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
   Fb += blockIdx.y * fb_stride;
   conv += blockIdx.y;
   if (!force && *conv) return;
-  __shared__ double sh[4];
+  __shared__ double sh[kRedWaves];
   const double* p = part + (int64_t)blockIdx.x * nblocks;
   double acc = 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += 256) acc += p[b];
-  // fixed-order butterfly inside each wave, then the 4 wave sums in order: deterministic
+  for (int b = threadIdx.x; b < nblocks; b += kRedThreads) acc += p[b];
+  // fixed-order butterfly inside each wave, then the wave sums in order: deterministic
   acc = butterfly_sum(acc, threadIdx.x & 63);   // = the xor-32 ... 1 shfl butterfly
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const double v = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+    double v = sh[0];
+    for (int w = 1; w < kRedWaves; ++w) v += sh[w];
     if (push.peers) p2p_push_values(push, blockIdx.x, &v, 1);
     else Fb[blockIdx.x] = v;
   }
@@ -1728,7 +1739,7 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
 // writes the next sweep's record of layer l.  Every input is loaded at the start.  The
 // convergence AND over layers rides on one arrival counter: each workgroup adds
 // 1 + 65536 * (layer not converged); the last to arrive sets iter / conv and rearms it.
-__global__ __launch_bounds__(256) void update_fused_kernel(UpdateArgs a) {
+__global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a) {
 #ifdef FREI_UPD_EMPTY  // diagnostic ablation build: launch floor
   return;
 #endif
@@ -1741,7 +1752,7 @@ __global__ __launch_bounds__(256) void update_fused_kernel(UpdateArgs a) {
   double* sTn = sh;                 // [nL] new T of layers l, l + 1 (the setup's T view)
   double* sP = sTn + nL;            // [nL] p of layers l, l + 1 (the setup's p view)
   double* sNodes = sP + nL;         // [n_tnodes] sorted T nodes
-  __shared__ double wsum[4][8];
+  __shared__ double wsum[kRedWaves][8];
   __shared__ double tot[8];         // this rank's sums of steps k0 (0..3) and k1 (4..7)
   __shared__ PMeta sPm[kMaxFastS];  // layer l's metadata per species (setup)
   __shared__ SpecMeta sSp[kMaxFastS];
@@ -1796,7 +1807,7 @@ __global__ __launch_bounds__(256) void update_fused_kernel(UpdateArgs a) {
     double acc[8];
     for (int j = 0; j < 8; ++j) acc[j] = 0.0;
 #pragma unroll 2
-    for (int b = tid; b < a.nblocks; b += 256)
+    for (int b = tid; b < a.nblocks; b += kRedThreads)
       for (int j = 0; j < 8; ++j) acc[j] += pj[j][b];
     for (int j = 0; j < 8; ++j)
       acc[j] = butterfly_sum(acc[j], tid & 63);   // = the xor-32 ... 1 shfl butterfly
@@ -1805,7 +1816,7 @@ __global__ __launch_bounds__(256) void update_fused_kernel(UpdateArgs a) {
   }
   // stage the setup's inputs in LDS (their loads were issued at the start)
   if (tid < ntn) sNodes[tid] = rNode;
-  for (int q = tid + 256; q < ntn; q += 256) sNodes[q] = a.su.tnodes[q];
+  for (int q = tid + kRedThreads; q < ntn; q += kRedThreads) sNodes[q] = a.su.tnodes[q];
   if (kn >= 0) {
     const int s = tid - 64;
     if (stage && s >= 0 && s < S) {
@@ -1817,7 +1828,11 @@ __global__ __launch_bounds__(256) void update_fused_kernel(UpdateArgs a) {
     if (tid == 1 && l + 1 < nL) sTn[l + 1] = T1;      // layer l + 1 before its update
   }
   __syncthreads();
-  if (tid < 8) tot[tid] = ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
+  if (tid < 8) {
+    double t = wsum[0][tid];
+    for (int w = 1; w < kRedWaves; ++w) t += wsum[w][tid];
+    tot[tid] = t;
+  }
   __syncthreads();
   const long long t0 = wall_clock64();
   if (a.p2p.mbox && tid == 64 && k0 >= 0) p2p_push_values(a.push, (int64_t)k0 * 4, tot, 4);
@@ -2265,7 +2280,7 @@ void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const
                    int64_t fb_stride, const P2PPush* push) {
   P2PPush p{};
   if (push) p = *push;
-  hipLaunchKernelGGL(reduce_kernel, dim3(n_idx, n_atm), dim3(256), 0, st, part, nblocks, Fb,
+  hipLaunchKernelGGL(reduce_kernel, dim3(n_idx, n_atm), dim3(kRedThreads), 0, st, part, nblocks, Fb,
                      conv, force, part_stride, fb_stride, p);
 }
 
@@ -2281,7 +2296,7 @@ void launch_update(const UpdateArgs& a, hipStream_t st, int n_atm) {
 
 void launch_update_fused(const UpdateArgs& a, hipStream_t st) {
   const size_t shm = (2 * (size_t)a.su.n_layers + a.su.n_tnodes) * sizeof(double);
-  hipLaunchKernelGGL(update_fused_kernel, dim3(a.su.n_layers), dim3(256), shm, st, a);
+  hipLaunchKernelGGL(update_fused_kernel, dim3(a.su.n_layers), dim3(kRedThreads), shm, st, a);
 }
 
 void launch_propagate(int64_t n, const double* c1, const double* lk, const double* F1u,
