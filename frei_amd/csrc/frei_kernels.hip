@@ -535,6 +535,18 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   auto top_of = [&](int k) { return DIR == kEmit && k == ns - 1; };
   auto load = [&](int k, double (&v)[2 * S], double& stale) {
     k = k < ns ? k : ns - 1;  // unconditional (clamped) loads keep vmcnt waits counted
+#ifdef FREI_CACHEONLY   // diagnostic build: same instructions, loads from a cache-resident 32 KB
+    {
+      const int64_t jj = j & 2047;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        v[2 * s] = stream_load(a.tab[s] + jj + (k & 1) * 2048);
+        v[2 * s + 1] = stream_load(a.tab[s] + jj + 4096);
+      }
+      stale = Fu[jj + (k & 1) * 2048];
+      return;
+    }
+#endif
     if constexpr (SH) {
       const int64_t off = uni(sp[k].off);
       const int layer = layer_of(k);

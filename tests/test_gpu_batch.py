@@ -147,3 +147,33 @@ def test_batched_emission_spectra_over_grids(fa):
         for t, sp_ in ((T, spec.flux), (T1, s1.flux)):
             assert rel(t, oT) <= max(1e-10, 2 * fT), (rel(t, oT), fT)
             assert rel(sp_, osp) <= max(1e-10, 2 * fS), (rel(sp_, osp), fS)
+
+
+@pytest.mark.parametrize("nc", [1, 4])
+def test_batched_pipe_sweep_matches_one_lane(fa, monkeypatch, nc):
+    """The producer/consumer sweep over (wavelength block, atmosphere) launches: with 4
+    consumers per block every atmosphere's T, spectrum and fluxes are bitwise those of the
+    one-lane sweep; with 1 only the block-sum tree of the bolometric partials differs."""
+    names = ["1H2-16O", "12C-16O", "Na"]
+    lam, p, tabs_o, tabs_f, g, mmr, T0 = _setup(fa, 3, 3000, 24, names, 23)
+    out = {}
+    monkeypatch.setenv("FREI_GROUP_Q", "1")
+    for v in (0, nc):
+        monkeypatch.setenv("FREI_PIPE", str(v))
+        eng = fa.BatchEngine(lam, p, tabs_f, g=g, mmr=mmr)
+        try:
+            path = eng.path()
+            assert path["contracted"] and path["pipe"] == v, path
+            r = eng.run(T0, n_timesteps=6, n_zero_crossings=10 ** 6, convergence_dT=-1.0)
+            out[v] = (r, eng.get_fluxes())
+        finally:
+            eng.close()
+    (r0, (u0, d0)), (r1, (u1, d1)) = out[0], out[nc]
+    assert np.array_equal(r0["n_iter"], r1["n_iter"])
+    if nc == 4:
+        assert np.array_equal(r1["final_T"], r0["final_T"])
+        assert np.array_equal(r1["spectra"], r0["spectra"])
+        assert np.array_equal(u1, u0) and np.array_equal(d1, d0)
+    else:
+        assert rel(r1["final_T"], r0["final_T"]) < 1e-12
+        assert row_normwise(r1["spectra"], r0["spectra"]) < 1e-9
