@@ -524,7 +524,10 @@ def main():
     if os.path.exists(vpath) and traffic is not None:
         valu = json.load(open(vpath))
 
-    c5 = None if a.no_c5 else c5_leg(a, d)
+    # C5 holds one contracted table per atmosphere (~31 GB per rank at its default size): with
+    # several ranks sharing one GPU (the rehearsal) it would not fit, so it is left out there
+    shared_gpu = d.world > n_dev
+    c5 = None if (a.no_c5 or shared_gpu) else c5_leg(a, d)
     binning = None
     if d.rank == 0 and not a.no_binning:
         binning = binning_leg(a, d.local, cpu=(d.world == 1 and not a.no_cpu_baseline))

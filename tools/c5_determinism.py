@@ -1,0 +1,37 @@
+"""Determinism check of the batched (C5) path: the bench's C5 workload run to radiative
+equilibrium three times in one process; prints per-run iteration counts and a hash of the
+final temperatures and spectra.  python tools/c5_determinism.py [n_lam] [mh]"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from frei_amd.batch import BatchEngine          # noqa: E402
+from frei_amd.opacity import SeparableTable     # noqa: E402
+from frei_amd.tp import temperature_grid        # noqa: E402
+from frei_amd.workloads import c3               # noqa: E402
+
+n_lam = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+mh = float(sys.argv[2]) if len(sys.argv) > 2 else -1.0
+w = c3(n_layers=60, n_lam=n_lam, n_T=16)
+T_refs = np.arange(1000.0, 2401.0, 200.0)
+loggs = np.array([2.5, 3.0, 3.5, 4.0])
+T0 = np.array([temperature_grid(w["p"], t, 0.1, 0.1) for t in T_refs for _ in loggs])
+g = np.array([10.0 ** lg for _ in T_refs for lg in loggs])
+T_nodes = np.linspace(0.8 * T0.min(), 1.2 * T0.max(), 16)
+fT = (T_nodes / 1000.0) ** 0.5
+tabs = {n: SeparableTable(w["base"][s], w["fp"][s], fT, w["p"], T_nodes)
+        for s, n in enumerate(w["names"])}
+mmr = np.broadcast_to(w["mmr"] * 10.0 ** mh, (len(g),) + w["mmr"].shape)
+eng = BatchEngine(w["lam"], w["p"], tabs, g=g, mmr=mmr, device=0)
+try:
+    eng.state_init(T0)
+    eng.iterate(6)
+    for r in range(3):
+        out = eng.run(T0, n_timesteps=200, n_zero_crossings=2, convergence_dT=3.0)
+        h = hashlib.sha1(out["final_T"].tobytes() + out["spectra"].tobytes()).hexdigest()[:12]
+        print(f"run {r}: n_iter {out['n_iter'].tolist()} hash {h}", flush=True)
+finally:
+    eng.close()
