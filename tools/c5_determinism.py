@@ -1,6 +1,9 @@
 """Determinism check of the batched (C5) path: the bench's C5 workload run to radiative
 equilibrium three times in one process; prints per-run iteration counts and a hash of the
-final temperatures and spectra.  python tools/c5_determinism.py [n_lam] [mh]"""
+final temperatures and spectra.  With a third argument G > 0, G GiB of device memory are
+first filled with 0xFF bytes (NaN doubles) and freed, so any read of memory the engine did not
+initialise would show up as changed results.
+    python tools/c5_determinism.py [n_lam] [mh] [G]"""
 import hashlib
 import os
 import sys
@@ -15,6 +18,21 @@ from frei_amd.workloads import c3               # noqa: E402
 
 n_lam = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 mh = float(sys.argv[2]) if len(sys.argv) > 2 else -1.0
+dirty_gib = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+if dirty_gib > 0:
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipSetDevice(0)
+    bufs = []
+    for _ in range(dirty_gib // 8):   # 8 GiB pieces, all live at once, then freed
+        b = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(b), ctypes.c_size_t(8 << 30)) == 0
+        assert hip.hipMemset(b, 0xFF, ctypes.c_size_t(8 << 30)) == 0
+        bufs.append(b)
+    hip.hipDeviceSynchronize()
+    for b in bufs:
+        hip.hipFree(b)
+    print(f"dirtied and freed {dirty_gib} GiB", flush=True)
 w = c3(n_layers=60, n_lam=n_lam, n_T=16)
 T_refs = np.arange(1000.0, 2401.0, 200.0)
 loggs = np.array([2.5, 3.0, 3.5, 4.0])
