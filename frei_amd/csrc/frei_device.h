@@ -271,6 +271,11 @@ struct FastArgs {
   int n_atm;               // atmospheres in the launch (0 or 1: a single atmosphere)
   int red_rows;            // one-lane sweep: per-row partial sums in LDS (fits: few layers)
   int unit_mmr;            // S = 1 with mmr = 1 everywhere (the contracted table, K3)
+  // rec_on: the sweep forms its own step records from the current temperatures in its
+  // prologue (contracted table, shared brackets, fixed mmr) instead of reading the ones the
+  // previous update kernel wrote; rec holds the setup inputs (T of this sweep).
+  int rec_on;
+  SetupArgs rec;
 };
 
 struct SweepArgs {

@@ -483,6 +483,47 @@ __host__ __device__ inline int64_t red_lds_doubles(int red_rows, int ns) {
   return (int64_t)red_rows_per_block(red_rows) * ns * 4 + (red_rows == 2 ? kStageDoubles : 0);
 }
 
+// The sweep's step records formed in its own prologue (FastArgs.rec_on: contracted table,
+// shared brackets, fixed mmr) from the temperatures the previous update kernel left: T, p and
+// the sorted T nodes are staged in `scratch` (LDS), then thread k forms record k into `dst`
+// (LDS) with setup_sweep's expressions — the records the update kernel would have written, bit
+// for bit, without that kernel's record step on the critical path.  Ends with a block barrier.
+__device__ __forceinline__ void step_s_core(const SetupArgs& u, const double* T, const double* P,
+                                            const double* tnodes, const SpecMeta& sm,
+                                            const PMeta& pm, int dir, int k, FastStepS& f);
+__device__ inline void atm_view(SetupArgs& u, int m);
+__host__ __device__ inline int64_t rec_scratch_doubles(const FastArgs& a) {
+  return a.rec_on ? 2 * (int64_t)a.rec.n_layers + a.rec.n_tnodes : 0;
+}
+__device__ __forceinline__ void stage_records(const FastArgs& a, int dir, FastStepS* dst,
+                                           double* scratch) {
+  SetupArgs u = a.rec;
+  if (a.n_atm > 1) atm_view(u, blockIdx.y);
+  const int nL = u.n_layers, ns = nL - 1, ntn = u.n_tnodes;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  double* sT = scratch;
+  double* sP = sT + nL;
+  double* sN = sP + nL;
+  for (int q = tid; q < nL; q += nthr) {
+    sT[q] = u.T[q];
+    sP[q] = u.p[q];
+  }
+  for (int q = tid; q < ntn; q += nthr) sN[q] = u.tnodes[q];
+  // this thread's first record's metadata, loaded with T / p (one global round trip in all)
+  const SpecMeta sm = u.spec[0];
+  const PMeta pm0 = u.pmeta[step_layer(dir, tid < ns ? tid : 0, nL)];
+  __syncthreads();
+  for (int k = tid; k < ns; k += nthr) {
+    FastStepS f;
+    step_s_core(u, sT, sP, sN, sm, k == tid ? pm0 : u.pmeta[step_layer(dir, k, nL)], dir, k,
+                f);
+    f.mmr[0] = 1.0;   // the contracted table's unit mixing ratio (MM1: never read)
+    for (int s = 1; s < kMaxFastS; ++s) f.mmr[s] = 0.0;
+    dst[k] = f;
+  }
+  __syncthreads();
+}
+
 template <int DIR, int S, int PD, bool NANCHK, bool SH, bool MM1>
 __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     FastArgs a, const FastStep* __restrict__ st, const FastStepS* __restrict__ ss,
@@ -521,10 +562,14 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   const FastStepS* sp = ss;
   if constexpr (SH) {
     double* lss = red + red_lds_doubles(a.red_rows, ns);
-    const double* g = reinterpret_cast<const double*>(ss);
     constexpr int kW = sizeof(FastStepS) / sizeof(double);
-    for (int idx = tid; idx < ns * kW; idx += kBlock) lss[idx] = g[idx];
-    __syncthreads();
+    if (a.rec_on) {   // form the records here from the current T (the update wrote none)
+      stage_records(a, DIR, reinterpret_cast<FastStepS*>(lss), lss + ns * kW);
+    } else {
+      const double* g = reinterpret_cast<const double*>(ss);
+      for (int idx = tid; idx < ns * kW; idx += kBlock) lss[idx] = g[idx];
+      __syncthreads();
+    }
     sp = reinterpret_cast<const FastStepS*>(lss);
   }
   // Load the 2S table rows and the stale opposite-stream flux of step k into one buffer
@@ -810,10 +855,14 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   const double* __restrict__ tab = a.tab[0];
   double* lss = red + red_lds_doubles(a.red_rows, ns);
   {
-    const double* g = reinterpret_cast<const double*>(ss);
     constexpr int kW = sizeof(FastStepS) / sizeof(double);
-    for (int idx = tid; idx < ns * kW; idx += kBlock) lss[idx] = g[idx];
-    __syncthreads();
+    if (a.rec_on) {   // form the records here from the current T (the update wrote none)
+      stage_records(a, DIR, reinterpret_cast<FastStepS*>(lss), lss + ns * kW);
+    } else {
+      const double* g = reinterpret_cast<const double*>(ss);
+      for (int idx = tid; idx < ns * kW; idx += kBlock) lss[idx] = g[idx];
+      __syncthreads();
+    }
   }
   const FastStepS* sp = reinterpret_cast<const FastStepS*>(lss);
   auto clampk = [&](int k) { return k < ns ? k : ns - 1; };
@@ -1024,7 +1073,8 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
 // Q lanes per wavelength: kBlock / Q wavelengths per block.
 void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStream_t st) {
   const size_t shm = (size_t)red_lds_doubles(a.red_rows, a.n_steps) * sizeof(double) +
-                     (size_t)a.n_steps * sizeof(FastStepS);
+                     (size_t)a.n_steps * sizeof(FastStepS) +
+                     (size_t)rec_scratch_doubles(a) * sizeof(double);
   const dim3 grid(nblocks, a.n_atm > 1 ? a.n_atm : 1);
   if (Q == 4) {
     if (dir == kEmit)
@@ -1067,9 +1117,10 @@ void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStrea
 // through scalar loads.
 constexpr int kPipeP = 3;    // producer waves per consumer wave
 constexpr int kPipeNV = 5;   // psi, xi, ic, Xu, Xd
+constexpr int kStepDoubles = (int)(sizeof(FastStepS) / sizeof(double));
 __host__ __device__ inline int64_t pipe_lds_doubles(int NC, int M, int ns) {
   return (int64_t)NC * 2 * (kPipeP * M) * kPipeNV * 64 + (int64_t)NC * 2 * 4 * kStageRow +
-         (int64_t)NC * ns * 4;
+         (int64_t)NC * ns * 4 + (int64_t)ns * kStepDoubles;
 }
 
 template <int DIR, int NC, int M, int PF>
@@ -1110,6 +1161,17 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
   double* ring = lds + (int64_t)sub * 2 * G * kPipeNV * 64;
   double* tile = lds + (int64_t)NC * 2 * G * kPipeNV * 64;   // [sub][2][4][kStageRow]
   double* red = tile + (int64_t)NC * 2 * 4 * kStageRow;      // [sub][ns][4]
+  // the step records in LDS: formed here from the current T (a.rec_on, scratch in the ring,
+  // which is not in use yet) or copied from the global step table
+  FastStepS* lrec = reinterpret_cast<FastStepS*>(red + (int64_t)NC * ns * 4);
+  if (a.rec_on) {
+    stage_records(a, DIR, lrec, lds);
+  } else {
+    const double* g = reinterpret_cast<const double*>(ss);
+    double* l = reinterpret_cast<double*>(lrec);
+    for (int idx = tid; idx < ns * kStepDoubles; idx += 256 * NC) l[idx] = g[idx];
+    __syncthreads();
+  }
   auto rslot = [&](int ph, int s, int v) {
     return ring + ((((ph & 1) * G + s) * kPipeNV + v) << 6) + lane;
   };
@@ -1126,11 +1188,11 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
     };
     auto load = [&](int ph, Buf& b) {
       const int kb = min(ph * G + p * M, ns - 1);
-      b.iT0 = (DIR == kEmit) ? ss[kb].iT1 : ss[kb].iT2;
+      b.iT0 = (DIR == kEmit) ? lrec[kb].iT1 : lrec[kb].iT2;
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const int k = min(ph * G + p * M + i, ns - 1);
-        const FastStepS& st = ss[k];
+        const FastStepS& st = lrec[k];
         const double* r = tabj + st.off;
         b.vlo[i] = stream_load(r);
         b.vhi[i] = stream_load(r + a.pitch);
@@ -1286,6 +1348,7 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
 template <int DIR, int NC, int M, int PF>
 static void launch_pipe_t(const FastArgs& a, int nblocks, hipStream_t st) {
   const size_t shm = (size_t)pipe_lds_doubles(NC, M, a.n_steps) * sizeof(double);
+  // (the record scratch reuses the LDS ring, which holds far more than 2 n_layers + n_tnodes)
   // dynamic LDS above 64 KiB needs the kernel's opt-in, raised whenever a launch needs more
   // (deeper atmospheres: the partial-sum rows grow with the step count)
   static size_t attr = 0;
@@ -1433,6 +1496,29 @@ void launch_log_ratio(const double* p, double p_top2, int nL, double* lnp, hipSt
 }
 
 // ---------------------------------------------------------------- setup (T -> terms)
+// Shared-bracket step record k of direction `dir` from temperatures T and pressures P (every
+// field but the mixing ratios): twostream.py:356-363 (T_1, T_2, p_2 of the top layer), :227-231
+// (dm), opacity.py:250-263 (the T bracket and weights).  Used by setup_sweep and by the sweeps
+// that form their own records (stage_records).
+__device__ __forceinline__ void step_s_core(const SetupArgs& u, const double* T, const double* P,
+                                            const double* tnodes, const SpecMeta& sm,
+                                            const PMeta& pm, int dir, int k, FastStepS& f) {
+  const int nL = u.n_layers;
+  const int i = step_layer(dir, k, nL);
+  const int top = (dir == kEmit && i == nL - 1) ? 1 : 0;
+  f.layer = i;
+  f.top = top;
+  f.iT1 = 1.0 / T[i];
+  f.iT2 = top ? f.iT1 : 1.0 / T[i + 1];
+  const double p2 = top ? u.p_top2 : P[i + 1];
+  f.dm = (P[i] - p2) / u.g;
+  int64_t off;
+  double wlo, whi;
+  fast_term(sm, pm, tnodes, T[i], off, wlo, whi);
+  f.off = off;
+  f.wlo = wlo;
+  f.whi = whi;
+}
 // Step records [kb, ke) of the sweep in direction `dir` from temperatures T (only the layers
 // of those steps and the ones above them are read), written by the threads tid = 0, 1, ...
 // of the caller's group (nthr of them).  pmeta / mmr of species s at layer i are read at
@@ -1455,19 +1541,7 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
     for (int k = kb + tid; k < ke; k += nthr) {
       const int i = step_layer(dir, k, nL);
       FastStepS* f = u.ssteps + k;
-      const int top = (dir == kEmit && i == nL - 1) ? 1 : 0;
-      f->layer = i;
-      f->top = top;
-      f->iT1 = 1.0 / T[i];
-      f->iT2 = top ? f->iT1 : 1.0 / T[i + 1];
-      const double p2 = top ? u.p_top2 : P[i + 1];
-      f->dm = (P[i] - p2) / u.g;
-      int64_t off;
-      double wlo, whi;
-      fast_term(spec[0], pmeta[MI(0, i)], tnodes, T[i], off, wlo, whi);
-      f->off = off;
-      f->wlo = wlo;
-      f->whi = whi;
+      step_s_core(u, T, P, tnodes, spec[0], pmeta[MI(0, i)], dir, k, *f);
       for (int s = 0; s < kMaxFastS; ++s) f->mmr[s] = s < nS ? MMR(s, i) : 0.0;
     }
     return;
@@ -2221,7 +2295,9 @@ void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream
 template <int DIR, int S, int PD, bool NC, bool SH, bool MM1 = false>
 static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
   const size_t shm = (size_t)red_lds_doubles(a.red_rows, a.n_steps) * sizeof(double) +
-                     (SH ? (size_t)a.n_steps * sizeof(FastStepS) : 0);
+                     (SH ? (size_t)a.n_steps * sizeof(FastStepS) +
+                               (size_t)rec_scratch_doubles(a) * sizeof(double)
+                         : 0);
   hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC, SH, MM1>),
                      dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1), dim3(kBlock), shm,
                      st, a, a.steps, a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);

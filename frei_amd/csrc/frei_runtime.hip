@@ -193,6 +193,8 @@ struct frei_ctx {
   int pipe_max_blocks = -1;             // blocks per GPU where the auto choice takes NC = 4
                                         // (-1: the CU count, one 16-wave block per CU)
   int n_cu = 256;                       // hipDeviceProp multiProcessorCount
+  int rec_sweep = 1;                    // FREI_REC_SWEEP: sweeps form their own step records
+  bool rec_skipped = false;             // the last update wrote no records (the sweep did)
   int pipe_m = 2;                       // steps per producer and phase
   int pipe_pf = 1;                      // FREI_PIPE_PF: phases the producers load ahead (1, 2)
   int red_rows = 1;                     // FREI_RED_ROWS=0: full wave sums per step
@@ -469,6 +471,15 @@ int pipe_consumers(frei_ctx* c) {
   return nc;
 }
 
+SetupArgs setup_args(frei_ctx* c);
+
+// Sweeps form their own step records in their prologue (and the update kernels skip writing
+// them) when the sweep reads the shared-bracket records from LDS — every form on the contracted
+// table with shared brackets — and the mixing ratios are fixed (no T-dependent chemistry).
+bool records_in_sweep(frei_ctx* c) {
+  return c->rec_sweep && c->fast && c->eff && c->shared && !c->chem_on;
+}
+
 SetupArgs setup_args(frei_ctx* c) {
   SetupArgs u{};
   u.n_layers = c->nL;
@@ -567,6 +578,14 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     HIP_TRY(hipEventRecord(e0, c->stream));
   }
   int nb_run = c->nblocks;  // partial-sum columns written by this sweep
+  const bool rec_on = c->fast && records_in_sweep(c);
+  // a sweep that reads the update's records after one whose update skipped them (an option or
+  // the tables changed mid-run): write this sweep's records first
+  if (!rec_on && c->rec_skipped && !c->dry) {
+    launch_setup(setup_args(c), o.dir, c->stream, c->n_atm);
+    HIP_TRY(hipGetLastError());
+  }
+  c->rec_skipped = false;
   if (c->fast) {
     FastArgs f{};
     f.n_lam = c->nlam;
@@ -592,6 +611,8 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     f.bs = atm_stride(c);
     f.n_atm = c->n_atm;
     f.unit_mmr = c->eff ? 1 : 0;
+    f.rec_on = rec_on ? 1 : 0;
+    if (f.rec_on) f.rec = setup_args(c);   // T of this sweep: c->d_T now
     // per-row partials while the one-lane sweep's LDS stays within 48 KiB (3+ blocks per CU)
     f.red_rows = c->red_rows &&
                  (size_t)16 * ns * 4 * sizeof(double) + (size_t)ns * sizeof(FastStepS) <=
@@ -700,6 +721,10 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   u.p2p = wait;
   u.dir = o.dir;
   u.next_dir = o.next_dir;
+  if (c->fast && records_in_sweep(c) && o.next_dir >= 0) {   // the next sweep forms its own
+    u.next_dir = -1;
+    c->rec_skipped = true;
+  }
   u.nranks = c->nranks;
   u.force = o.force;
   u.track = o.track;
@@ -798,7 +823,7 @@ bool ready(frei_ctx* c) { return c && c->grid_set; }
 const char* const kOptionNames[] = {"prefetch_depth", "shared", "shared_max_blocks",
                                     "precontract", "depth4_max_blocks", "pair_max_blocks",
                                     "quad_max_blocks", "red_rows", "red_stage", "group_q",
-                                    "fused_update", "graph", "pipe", "pipe_pf", "pipe_min_blocks",
+                                    "fused_update", "graph", "pipe", "pipe_pf", "pipe_min_blocks", "rec_sweep",
                                     "pipe_max_blocks", nullptr};
 int set_option(frei_ctx* c, const std::string& k, int v) {
   if (k == "prefetch_depth") c->prefetch_depth = v;
@@ -815,6 +840,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "graph") c->use_graph = v != 0;
   else if (k == "pipe") c->pipe_nc = (v == 1 || v == 2 || v == 4 || v == -1) ? v : 0;
   else if (k == "pipe_min_blocks") c->pipe_min_blocks = v;
+  else if (k == "rec_sweep") c->rec_sweep = v != 0;
   else if (k == "pipe_max_blocks") c->pipe_max_blocks = v;
   else if (k == "pipe_pf") c->pipe_pf = v == 1 ? 1 : 2;
   else return fail("unknown option '" + k + "'");

@@ -543,9 +543,9 @@ def test_grouped_lane_sweep_matches_one_lane_form(fa, monkeypatch, n_layers, red
         assert row_normwise(out[q]["run"]["spectrum"], out[1]["run"]["spectrum"]) < 1e-9
 
 
-# 33 / 36 / 59 / 99 steps: partial phases; 100 layers needs more LDS than the earlier cases
+# 33 / 36 / 59 / 79 steps: partial phases; 80 layers needs more LDS than the earlier cases
 # (the kernel's dynamic-LDS opt-in is raised between launches)
-@pytest.mark.parametrize("n_layers", [34, 37, 60, 100])
+@pytest.mark.parametrize("n_layers", [34, 37, 60, 80])
 def test_pipe_sweep_matches_one_lane_form(fa, monkeypatch, n_layers):
     """The producer/consumer sweep (three producer waves form the step coefficients into an LDS
     ring, one consumer wave runs the carried chain) uses the one-lane expressions in the same
@@ -601,6 +601,43 @@ def test_pipe_sweep_matches_one_lane_form(fa, monkeypatch, n_layers):
         else:
             assert rel(rp["final_T"], ro["final_T"]) < 1e-12
             assert row_normwise(rp["spectrum"], ro["spectrum"]) < 1e-9
+
+
+@pytest.mark.parametrize("form", [("1", "0"), ("2", "0"), ("4", "0"), ("1", "4"), ("1", "1")])
+def test_step_records_formed_in_sweep_are_bitwise_the_updates(fa, monkeypatch, form):
+    """With shared brackets on the contracted table the sweeps form their own step records from
+    the current temperatures (FREI_REC_SWEEP, default on) and the update kernel writes none: a
+    T-P run gives bitwise the temperatures, spectrum, fluxes and dtaus of the update-written
+    records, in every sweep form (one-lane with LDS records, two / four lanes per wavelength,
+    producer/consumer with 4 and 1 consumers)."""
+    q, nc = form
+    rng = np.random.default_rng(5)
+    lam, _, _ = O.wavelength_grid(0.5, 10, 3000)
+    nL = 33
+    p = O.pressure_grid(nL, -6, np.log10(200))
+    T0 = O.temperature_grid(p, 1600.0, 0.1, 0.1)
+    Tn = np.linspace(0.8 * T0.min(), 1.2 * T0.max(), 9)
+    names = ["1H2-16O", "12C-16O"]
+    tabs = {n: fa.SeparableTable(10 ** rng.uniform(-4, 2, lam.size), (p / 1.0) ** 0.1,
+                                 (Tn / 1000.0) ** 0.5, p, Tn) for n in names}
+    mmr = O.mock_mmr(names, M_BAR)[:, None] * np.ones(nL)
+    monkeypatch.setenv("FREI_GROUP_Q", q)
+    monkeypatch.setenv("FREI_PIPE", nc)
+    out = {}
+    for rec in ("0", "1"):
+        monkeypatch.setenv("FREI_REC_SWEEP", rec)
+        eng = fa.Engine(lam, p, tabs, mmr=mmr)
+        try:
+            path = eng.path()
+            assert path["contracted"] and path["lds_steps"] and path["pipe"] == int(nc)
+            r = eng.run(T0, n_timesteps=5, n_zero_crossings=10 ** 6, convergence_dT=-1.0)
+            out[rec] = (r, eng.get_fluxes())
+        finally:
+            eng.close()
+    (a, fa_), (b, fb_) = out["0"], out["1"]
+    for k in ("final_T", "spectrum", "dtaus", "temp_hist"):
+        assert np.array_equal(a[k], b[k]), k
+    assert all(np.array_equal(x, y) for x, y in zip(fa_, fb_))
 
 
 def test_shims_reuse_device_context_and_vector_kappa(fa, golden):
