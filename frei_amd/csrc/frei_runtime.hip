@@ -193,7 +193,9 @@ struct frei_ctx {
   int pipe_max_blocks = -1;             // blocks per GPU where the auto choice takes NC = 4
                                         // (-1: the CU count, one 16-wave block per CU)
   int n_cu = 256;                       // hipDeviceProp multiProcessorCount
-  int rec_sweep = 1;                    // FREI_REC_SWEEP: sweeps form their own step records
+  int rec_sweep = -1;                   // FREI_REC_SWEEP: sweeps form their own step records
+                                        // (1 every form, 0 never, -1 not the producer/consumer
+                                        // sweep, where it measured neutral to slower)
   bool rec_skipped = false;             // the last update wrote no records (the sweep did)
   int pipe_m = 2;                       // steps per producer and phase
   int pipe_pf = 1;                      // FREI_PIPE_PF: phases the producers load ahead (1, 2)
@@ -477,7 +479,8 @@ SetupArgs setup_args(frei_ctx* c);
 // them) when the sweep reads the shared-bracket records from LDS — every form on the contracted
 // table with shared brackets — and the mixing ratios are fixed (no T-dependent chemistry).
 bool records_in_sweep(frei_ctx* c) {
-  return c->rec_sweep && c->fast && c->eff && c->shared && !c->chem_on;
+  if (!(c->rec_sweep && c->fast && c->eff && c->shared && !c->chem_on)) return false;
+  return c->rec_sweep > 0 || pipe_consumers(c) == 0;
 }
 
 SetupArgs setup_args(frei_ctx* c) {
@@ -840,7 +843,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "graph") c->use_graph = v != 0;
   else if (k == "pipe") c->pipe_nc = (v == 1 || v == 2 || v == 4 || v == -1) ? v : 0;
   else if (k == "pipe_min_blocks") c->pipe_min_blocks = v;
-  else if (k == "rec_sweep") c->rec_sweep = v != 0;
+  else if (k == "rec_sweep") c->rec_sweep = v < 0 ? -1 : (v ? 1 : 0);
   else if (k == "pipe_max_blocks") c->pipe_max_blocks = v;
   else if (k == "pipe_pf") c->pipe_pf = v == 1 ? 1 : 2;
   else return fail("unknown option '" + k + "'");

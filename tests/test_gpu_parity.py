@@ -606,7 +606,8 @@ def test_pipe_sweep_matches_one_lane_form(fa, monkeypatch, n_layers):
 @pytest.mark.parametrize("form", [("1", "0"), ("2", "0"), ("4", "0"), ("1", "4"), ("1", "1")])
 def test_step_records_formed_in_sweep_are_bitwise_the_updates(fa, monkeypatch, form):
     """With shared brackets on the contracted table the sweeps form their own step records from
-    the current temperatures (FREI_REC_SWEEP, default on) and the update kernel writes none: a
+    the current temperatures (FREI_REC_SWEEP; by default in every form but the producer/consumer
+    sweep, forced here for all) and the update kernel writes none: a
     T-P run gives bitwise the temperatures, spectrum, fluxes and dtaus of the update-written
     records, in every sweep form (one-lane with LDS records, two / four lanes per wavelength,
     producer/consumer with 4 and 1 consumers)."""
@@ -625,7 +626,7 @@ def test_step_records_formed_in_sweep_are_bitwise_the_updates(fa, monkeypatch, f
     monkeypatch.setenv("FREI_PIPE", nc)
     out = {}
     for rec in ("0", "1"):
-        monkeypatch.setenv("FREI_REC_SWEEP", rec)
+        monkeypatch.setenv("FREI_REC_SWEEP", rec)   # 1: every form (the default skips the pipe)
         eng = fa.Engine(lam, p, tabs, mmr=mmr)
         try:
             path = eng.path()
