@@ -243,6 +243,16 @@ template <typename T>
 int dalloc(T** p, size_t n) {
   if (n == 0) n = 1;
   HIP_TRY(hipMalloc((void**)p, n * sizeof(T)));
+  // FREI_ALLOC_FILL (diagnostic): fill every new device buffer with a byte value, so a read of
+  // memory the engine never wrote shows up as changed results
+  static const int fill = [] {
+    const char* e = getenv("FREI_ALLOC_FILL");
+    return e ? atoi(e) : -1;
+  }();
+  if (fill >= 0) {   // (the null-stream memset must finish before the context's stream uses p)
+    HIP_TRY(hipMemset((void*)*p, fill, n * sizeof(T)));
+    HIP_TRY(hipDeviceSynchronize());
+  }
   return 0;
 }
 
@@ -255,6 +265,9 @@ void dfree(T*& p) {
 template <typename T>
 int h2d(T* d, const T* h, size_t n, hipStream_t st) {
   HIP_TRY(hipMemcpyAsync(d, h, n * sizeof(T), hipMemcpyHostToDevice, st));
+  // the sources are often temporaries (pageable, freed at the caller's scope exit): wait for
+  // the copy (setup and per-run uploads only, never inside the T-P loop)
+  HIP_TRY(hipStreamSynchronize(st));
   return 0;
 }
 
@@ -940,11 +953,13 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
   for (int k = 0; k < 2; ++k)
     if (hipEventCreateWithFlags(&c->flag_ev[k], hipEventDisableTiming) != hipSuccess)
       return bail(fail("hipEventCreate failed"));
-  if (hipMemset(c->d_Fu, 0, F * sizeof(double)) != hipSuccess ||
-      hipMemset(c->d_Fd, 0, F * sizeof(double)) != hipSuccess ||
-      hipMemset(c->d_conv, 0, sizeof(int) * A) != hipSuccess ||
-      hipMemset(c->d_done, 0, sizeof(unsigned)) != hipSuccess)
-    return bail(fail("hipMemset failed"));
+  // stream-ordered (the context's stream does not synchronise with the null stream)
+  if (hipMemsetAsync(c->d_Fu, 0, F * sizeof(double), c->stream) != hipSuccess ||
+      hipMemsetAsync(c->d_Fd, 0, F * sizeof(double), c->stream) != hipSuccess ||
+      hipMemsetAsync(c->d_conv, 0, sizeof(int) * A, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->d_done, 0, sizeof(unsigned), c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return bail(fail("hipMemsetAsync failed"));
   if (A > 1 && hipHostMalloc((void**)&c->h_conv, 2 * A * sizeof(int)) != hipSuccess)
     return bail(fail("hipHostMalloc failed"));
   *out = c;
@@ -1067,7 +1082,11 @@ static int set_table_common(frei_ctx* c, int s, const double* p_nodes, int n_p,
     dfree(q.d_tab);
     TRY(dalloc(&q.d_tab, need));
   }
-  HIP_TRY(hipMemset(q.d_tab, 0, need * sizeof(double)));  // finite padding
+  // finite padding; on the context's stream, ordered before the table upload / generation.
+  // (A null-stream hipMemset is not ordered with the non-blocking stream: it could still be
+  // zeroing the table while gen_table_kernel writes it — the intermittent C5 results of round 2.)
+  HIP_TRY(hipMemsetAsync(q.d_tab, 0, need * sizeof(double), c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));   // before frei_set_table's blocking host copies
   q.stride = stride;
   q.n_p = n_p;
   q.n_T = n_T;
@@ -1703,7 +1722,9 @@ int frei_comm_p2p_handle(frei_ctx* c, int nranks, int rank, void* handle64) {
   void* mb = nullptr;
   HIP_TRY(hipExtMallocWithFlags(&mb, mbox_bytes(nranks, n), hipDeviceMallocUncached));
   c->d_mbox = static_cast<double*>(mb);
-  HIP_TRY(hipMemset(c->d_mbox, 0, mbox_bytes(nranks, n)));   // flags 0: nothing published
+  // flags 0: nothing published; complete before the handle goes to the peers
+  HIP_TRY(hipMemsetAsync(c->d_mbox, 0, mbox_bytes(nranks, n), c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
   hipIpcMemHandle_t h;
   HIP_TRY(hipIpcGetMemHandle(&h, c->d_mbox));
   std::memcpy(handle64, &h, sizeof(h));
@@ -1858,7 +1879,7 @@ int frei_timing_enable(frei_ctx* c, int on) {
   c->ev_used = 0;
   c->xev_used = 0;
   if (c->d_wait_ticks)
-    HIP_TRY(hipMemset(c->d_wait_ticks, 0, sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(c->d_wait_ticks, 0, sizeof(unsigned long long), c->stream));
   return 0;
 }
 

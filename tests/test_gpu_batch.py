@@ -177,3 +177,39 @@ def test_batched_pipe_sweep_matches_one_lane(fa, monkeypatch, nc):
     else:
         assert rel(r1["final_T"], r0["final_T"]) < 1e-12
         assert row_normwise(r1["spectra"], r0["spectra"]) < 1e-9
+
+
+def test_tables_are_ordered_after_device_memory_reuse(fa):
+    """Table allocation zeroes the row padding on the context's stream, ordered before the
+    device-side table generation: a context whose tables land in memory another context just
+    freed gives bitwise the results of a fresh one.  (Round 2 found the padding memset on the
+    null stream, unordered with the context's non-blocking stream: it could still be zeroing a
+    table the generator had written, which changed C5 runs after other contexts.)"""
+    from frei_amd.workloads import c3
+    from frei_amd.engine import Engine
+
+    def batch_run():
+        w = c3(n_layers=60, n_lam=100_000, n_T=16)
+        tabs = {n: fa.SeparableTable(w["base"][s], w["fp"][s], w["fT"][s], w["p"], w["T_nodes"])
+                for s, n in enumerate(w["names"])}
+        A = 16
+        g = np.linspace(300.0, 10000.0, A)
+        T0 = np.array([w["T0"] * (0.85 + 0.3 * m / A) for m in range(A)])
+        mmr = np.broadcast_to(w["mmr"], (A,) + w["mmr"].shape)
+        eng = fa.BatchEngine(w["lam"], w["p"], tabs, g=g, mmr=mmr)
+        try:
+            return eng.run(T0, n_timesteps=12, n_zero_crossings=10 ** 6, convergence_dT=-1.0)
+        finally:
+            eng.close()
+
+    fresh = batch_run()
+    w3 = c3(n_lam=400_000)   # a large context created, iterated and freed in between
+    tabs3 = {n: fa.SeparableTable(w3["base"][s], w3["fp"][s], w3["fT"][s], w3["p"], w3["T_nodes"])
+             for s, n in enumerate(w3["names"])}
+    e3 = Engine(w3["lam"], w3["p"], tabs3, mmr=w3["mmr"])
+    e3.state_init(w3["T0"])
+    e3.iterate(3)
+    e3.close()
+    reused = batch_run()
+    assert np.array_equal(fresh["final_T"], reused["final_T"])
+    assert np.array_equal(fresh["spectra"], reused["spectra"])

@@ -3,7 +3,9 @@ equilibrium three times in one process; prints per-run iteration counts and a ha
 final temperatures and spectra.  With a third argument G > 0, G GiB of device memory are
 first filled with 0xFF bytes (NaN doubles) and freed, so any read of memory the engine did not
 initialise would show up as changed results.
-    python tools/c5_determinism.py [n_lam] [mh] [G]"""
+With a fourth argument "afterc3", a C3 context is created, run and closed first (the bench's
+order).
+    python tools/c5_determinism.py [n_lam] [mh] [G] [afterc3]"""
 import hashlib
 import os
 import sys
@@ -19,6 +21,19 @@ from frei_amd.workloads import c3               # noqa: E402
 n_lam = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 mh = float(sys.argv[2]) if len(sys.argv) > 2 else -1.0
 dirty_gib = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+after_c3 = len(sys.argv) > 4 and sys.argv[4] == "afterc3"
+if after_c3:   # the bench's order: a C3 context (30 GB of tables) created, iterated and closed first
+    from frei_amd.engine import Engine
+    w3 = c3()
+    tabs3 = {n: SeparableTable(w3["base"][s], w3["fp"][s], w3["fT"][s], w3["p"], w3["T_nodes"])
+             for s, n in enumerate(w3["names"])}
+    e3 = Engine(w3["lam"], w3["p"], tabs3, mmr=w3["mmr"], device=0)
+    e3.state_init(w3["T0"])
+    e3.iterate(5)
+    out3 = e3.run(w3["T0"], n_timesteps=50, n_zero_crossings=2, convergence_dT=3.0, want_dtaus=False)
+    e3.close()
+    del e3
+    print(f"C3 context created, run ({out3['n_iter']} iterations) and closed", flush=True)
 if dirty_gib > 0:
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so")
