@@ -343,6 +343,10 @@ def main():
             _pad = ctypes.c_void_p()
             hip.hipMalloc(ctypes.byref(_pad), ctypes.c_size_t((d.local // n_dev) * 1536 << 20))
         d.local = d.local % n_dev
+        # the producer/consumer sweep takes a whole CU per block (VGPRs and LDS); next to other
+        # ranks' update kernels spinning on the same GPU for their peers' sums its blocks can
+        # starve (a P2P timeout): ranks that share a GPU use the grouped-lane form instead
+        os.environ.setdefault("FREI_PIPE", "0")
     w = c3(n_layers=a.n_layers, n_lam=a.n_lam, n_T=a.n_T)
     nL, n_lam, S = a.n_layers, a.n_lam, len(w["names"])
     lo, hi = partition(n_lam, d.world, d.rank)
