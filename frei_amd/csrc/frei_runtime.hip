@@ -305,6 +305,7 @@ int build_contracted(frei_ctx* c, bool shared_fast, Lap&& lap) {
   const size_t per = (size_t)q0.n_p * q0.n_T * (size_t)q0.stride + 64;
   const size_t need = per * c->n_atm;
   if (c->eff_cap < need) {
+    HIP_TRY(hipStreamSynchronize(c->stream));   // no queued sweep still reads the old table
     dfree(c->d_eff);
     c->eff_cap = 0;
     TRY(dalloc(&c->d_eff, need));
@@ -437,6 +438,7 @@ int build_meta(frei_ctx* c) {
   const bool lds_fits =
       (size_t)(kBlock / 64) * ns_l * 4 * sizeof(double) + ns_l * sizeof(FastStepS) <= 64 * 1024;
   c->shared = (c->shared_mode == 1 || (c->shared_mode < 0 && small)) && lds_fits ? shared : 0;
+  HIP_TRY(hipStreamSynchronize(c->stream));   // queued kernels may still read the metadata
   dfree(c->d_smeta);
   dfree(c->d_pmeta);
   dfree(c->d_tnodes);
@@ -802,6 +804,7 @@ int reset_loop_state(frei_ctx* c) {
 
 int ensure_hist(frei_ctx* c, int cap) {
   if (cap <= c->hist_cap) return 0;
+  HIP_TRY(hipStreamSynchronize(c->stream));   // queued update kernels may still write it
   dfree(c->d_hist);
   TRY(dalloc(&c->d_hist, (size_t)cap * 2 * c->nL * c->n_atm));
   c->hist_cap = cap;
@@ -1078,6 +1081,8 @@ static int set_table_common(frei_ctx* c, int s, const double* p_nodes, int n_p,
   Species& q = c->sp[s];
   const int64_t stride = (c->nlam + 63) / 64 * 64;
   const size_t need = (size_t)n_p * n_T * (size_t)stride + 64;
+  // queued sweeps of the old tables must finish before they are overwritten or freed
+  HIP_TRY(hipStreamSynchronize(c->stream));
   if (!q.d_tab || (size_t)q.n_p * q.n_T != (size_t)n_p * n_T) {
     dfree(q.d_tab);
     TRY(dalloc(&q.d_tab, need));
