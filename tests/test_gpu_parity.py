@@ -543,9 +543,9 @@ def test_grouped_lane_sweep_matches_one_lane_form(fa, monkeypatch, n_layers, red
         assert row_normwise(out[q]["run"]["spectrum"], out[1]["run"]["spectrum"]) < 1e-9
 
 
-# 33 / 36 / 59 / 79 steps: partial phases; 80 layers needs more LDS than the earlier cases
-# (the kernel's dynamic-LDS opt-in is raised between launches)
-@pytest.mark.parametrize("n_layers", [34, 37, 60, 80])
+# 4 steps (one partial phase) / 33 / 36 / 59 / 79 steps: partial phases; 80 layers needs more
+# LDS than the earlier cases (the kernel's dynamic-LDS opt-in is raised between launches)
+@pytest.mark.parametrize("n_layers", [5, 34, 37, 60, 80])
 def test_pipe_sweep_matches_one_lane_form(fa, monkeypatch, n_layers):
     """The producer/consumer sweep (three producer waves form the step coefficients into an LDS
     ring, one consumer wave runs the carried chain) uses the one-lane expressions in the same
