@@ -194,8 +194,8 @@ struct frei_ctx {
                                         // (-1: the CU count, one 16-wave block per CU)
   int n_cu = 256;                       // hipDeviceProp multiProcessorCount
   int rec_sweep = -1;                   // FREI_REC_SWEEP: sweeps form their own step records
-                                        // (1 every form, 0 never, -1 not the producer/consumer
-                                        // sweep, where it measured neutral to slower)
+                                        // (1 every form, 0 never, -1 single-atmosphere contexts
+                                        // without the producer/consumer sweep)
   bool rec_skipped = false;             // the last update wrote no records (the sweep did)
   int pipe_m = 2;                       // steps per producer and phase
   int pipe_pf = 1;                      // FREI_PIPE_PF: phases the producers load ahead (1, 2)
@@ -495,7 +495,9 @@ SetupArgs setup_args(frei_ctx* c);
 // table with shared brackets — and the mixing ratios are fixed (no T-dependent chemistry).
 bool records_in_sweep(frei_ctx* c) {
   if (!(c->rec_sweep && c->fast && c->eff && c->shared && !c->chem_on)) return false;
-  return c->rec_sweep > 0 || pipe_consumers(c) == 0;
+  // auto: not for the producer/consumer sweep (neutral to slower) nor for batched contexts
+  // (every (block, atmosphere) would form the records: C5 -2 %, profiles/r02_ab_rec_sweep.txt)
+  return c->rec_sweep > 0 || (pipe_consumers(c) == 0 && c->n_atm == 1);
 }
 
 SetupArgs setup_args(frei_ctx* c) {
