@@ -1388,6 +1388,9 @@ size_t pipe_lds_bytes(int NC, int M, int ns) {
 }
 
 // ---------------------------------------------------------------- P2P exchange
+#ifndef FREI_P2P_FENCE
+#define FREI_P2P_FENCE 1
+#endif
 // System-scope stores of a value and then its flag into every rank's mailbox (P2PPush): the
 // release fence orders the value stores before the flag stores for any observer; the
 // explicit wait keeps the compiler from dropping the fence's completion wait (gfx950 hazard,
@@ -1401,7 +1404,13 @@ __device__ __forceinline__ void p2p_push_values(const P2PPush& p, int64_t idx, c
       __hip_atomic_store(dst + idx + k, __builtin_bit_cast(uint64_t, v[k]), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
+#if FREI_P2P_FENCE
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+#endif
+  // The system-scope release orders the value stores before the flag stores for any observer.
+  // (The payload is only the write-through system-scope stores above, so the completion wait
+  // alone would order them too; FREI_P2P_FENCE=0 drops the fence: measured no different,
+  // profiles/r02_p2p_after_fix.txt, so the canonical release stays.)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (int r = 0; r < p.nranks; ++r) {
     uint64_t* fl = reinterpret_cast<uint64_t*>(p.peers[r]) + mbox_flag(par, p.rank, p.nranks, p.n);
