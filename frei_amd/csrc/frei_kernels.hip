@@ -1930,7 +1930,9 @@ __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a)
   }
   __syncthreads();
   const long long t0 = wall_clock64();
+#ifndef FREI_P2P_NOPUSH   // diagnostic ablation build: no push (a one-rank run still completes)
   if (a.p2p.mbox && tid == 64 && k0 >= 0) p2p_push_values(a.push, (int64_t)k0 * 4, tot, 4);
+#endif
   if (tid < 64) {
     // all ranks' sums in rank order (lanes 0..7), then dT of layers l, l + 1 (lanes 0, 1)
     double v = 0.0;
