@@ -296,6 +296,23 @@ def build_engine(w, tabs, lo, hi, d, kind, force=False):
                   comm=comm)
 
 
+def build_engine_fallback(w, tabs, lo, hi, d, force, note):
+    """After a failed P2P setup: RCCL on every rank, or — when RCCL cannot be set up on some
+    rank either — the host all-gather over the socket rendezvous (slow, always available), so
+    the run still reports a line.  Returns (engine, kind, note)."""
+    eng, err = None, None
+    try:
+        eng = build_engine(w, tabs, lo, hi, d, "rccl", force)
+    except RuntimeError as e:
+        err = str(e)
+    if d.all_ok(eng is not None):
+        return eng, "rccl", note + "; fell back to RCCL"
+    if eng is not None:
+        eng.close()
+    return (build_engine(w, tabs, lo, hi, d, "host", force), "host",
+            note + f"; RCCL setup failed too ({err or 'on a peer rank'}): host all-gather")
+
+
 def timed_iterations(eng, d, warmup, steps):
     """Fixed-work T-P iterations: warm-up, then exactly ``steps`` bracketed by a barrier and a
     stream synchronize on both sides; the max over ranks."""
@@ -364,9 +381,8 @@ def main():
             raise SystemExit(f"rank {d.rank}: engine setup failed: {err}")
         if eng is not None:
             eng.close()
-        comm_note = f"p2p setup failed ({err or 'on a peer rank'}); fell back to RCCL"
-        kind = "rccl"
-        eng = build_engine(w, tabs, lo, hi, d, kind, a.force_comm)
+        eng, kind, comm_note = build_engine_fallback(
+            w, tabs, lo, hi, d, a.force_comm, f"p2p setup failed ({err or 'on a peer rank'})")
     tables_s = time.perf_counter() - t_e
     # one-time setup: metadata build + species contraction (K3), outside the timed steps
     t_s = time.perf_counter()
@@ -385,10 +401,9 @@ def main():
             err = str(e)
         if not d.all_ok(err is None):
             eng.close()
-            comm_note = f"p2p exchange failed at run time ({err or 'on a peer rank'}); " \
-                        "fell back to RCCL"
-            kind = "rccl"
-            eng = build_engine(w, tabs, lo, hi, d, kind, a.force_comm)
+            eng, kind, comm_note = build_engine_fallback(
+                w, tabs, lo, hi, d, a.force_comm,
+                f"p2p exchange failed at run time ({err or 'on a peer rank'})")
 
     # ---- headline: timed fixed-work T-P iterations (no per-kernel events inside)
     eng.state_init(w["T0"])

@@ -8,6 +8,7 @@ and calls the HIP kernels for sweeps, the T-P loop and kappa.  Nothing here comp
 fluxes on the CPU: without libfrei_hip.so every call raises.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -131,8 +132,13 @@ class Engine:
             N.check(lib.frei_comm_init(self._ctx, nranks, rank, buf))
         elif kind == "p2p":
             h = ctypes.create_string_buffer(64)
-            rc = lib.frei_comm_p2p_handle(self._ctx, nranks, rank, h)
-            msg = lib.frei_last_error().decode(errors="replace") if rc else ""
+            # FREI_FAULT_P2P=1: fault injection for the fallback tests (this rank's setup fails,
+            # it still joins the handle exchange so its peers fail too instead of hanging)
+            if os.environ.get("FREI_FAULT_P2P") == "1":
+                rc, msg = 1, "P2P setup failure injected (FREI_FAULT_P2P)"
+            else:
+                rc = lib.frei_comm_p2p_handle(self._ctx, nranks, rank, h)
+                msg = lib.frei_last_error().decode(errors="replace") if rc else ""
             hs = arg(h.raw if rc == 0 else b"")     # every rank joins the exchange
             if rc != 0:
                 raise RuntimeError(f"frei_hip: {msg}")
