@@ -213,3 +213,25 @@ def test_tables_are_ordered_after_device_memory_reuse(fa):
     reused = batch_run()
     assert np.array_equal(fresh["final_T"], reused["final_T"])
     assert np.array_equal(fresh["spectra"], reused["spectra"])
+
+
+def test_batched_step_records_formed_in_sweep_are_bitwise_the_updates(fa, monkeypatch):
+    """In-sweep step records forced on a batched context (FREI_REC_SWEEP=1; off by default for
+    batches): every (block, atmosphere) forms its atmosphere's records from that atmosphere's
+    T and gravity — bitwise the results of the update-written records."""
+    names = ["1H2-16O", "12C-16O", "Na"]
+    lam, p, tabs_o, tabs_f, g, mmr, T0 = _setup(fa, 4, 2500, 26, names, 29)
+    out = {}
+    for rec in ("0", "1"):
+        monkeypatch.setenv("FREI_REC_SWEEP", rec)
+        eng = fa.BatchEngine(lam, p, tabs_f, g=g, mmr=mmr)
+        try:
+            assert eng.path()["lds_steps"]
+            r = eng.run(T0, n_timesteps=8, n_zero_crossings=10 ** 6, convergence_dT=-1.0)
+            out[rec] = (r, eng.get_fluxes())
+        finally:
+            eng.close()
+    (a, fa_), (b, fb_) = out["0"], out["1"]
+    assert np.array_equal(a["final_T"], b["final_T"])
+    assert np.array_equal(a["spectra"], b["spectra"])
+    assert all(np.array_equal(x, y) for x, y in zip(fa_, fb_))
