@@ -289,11 +289,22 @@ def build_engine(w, tabs, lo, hi, d, kind, force=False):
     comm = None
     if d.world > 1 or force:
         rdzv = d.rdzv if d.rdzv is not None else Rendezvous(1, 0)
-        if force and kind == "rccl":
-            os.environ["FREI_FORCE_RCCL"] = "1"
         comm = {"p2p": p2p_comm, "rccl": rccl_comm, "host": host_comm}[kind](rdzv)
-    return Engine(w["lam"], w["p"], tabs, mmr=w["mmr"], device=d.local, lam_slice=(lo, hi),
-                  comm=comm)
+    # a forced one-rank RCCL communicator is requested through FREI_FORCE_RCCL for this
+    # engine's construction only (later engines of the run do not inherit it)
+    forced = force and kind == "rccl"
+    prev = os.environ.get("FREI_FORCE_RCCL")
+    if forced:
+        os.environ["FREI_FORCE_RCCL"] = "1"
+    try:
+        return Engine(w["lam"], w["p"], tabs, mmr=w["mmr"], device=d.local, lam_slice=(lo, hi),
+                      comm=comm)
+    finally:
+        if forced:
+            if prev is None:
+                os.environ.pop("FREI_FORCE_RCCL", None)
+            else:
+                os.environ["FREI_FORCE_RCCL"] = prev
 
 
 def build_engine_fallback(w, tabs, lo, hi, d, force, note):

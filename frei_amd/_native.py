@@ -100,6 +100,12 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"frei_amd: native library {LIB_PATH} is missing; build it with "
                                "`python -m frei_amd.build` (no CPU fallback exists)")
+        if LIB_PATH == _DEFAULT_LIB and os.environ.get("FREI_SKIP_STAMP") != "1":
+            from .build import stamp_matches
+            if not stamp_matches(LIB_PATH):
+                raise RuntimeError(f"frei_amd: {LIB_PATH} was not built from the sources in this "
+                                   "tree (its .stamp hash differs); rebuild with "
+                                   "`python -m frei_amd.build`")
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
         for name, (res, args) in SIGNATURES.items():
             if LIB_PATH != _DEFAULT_LIB and not hasattr(L, name):

@@ -1,5 +1,12 @@
-"""Build libfrei_hip.so in-tree for gfx950:  python -m frei_amd.build"""
+"""Build libfrei_hip.so in-tree for gfx950:  python -m frei_amd.build
+
+The library is rebuilt whenever the SHA-256 of its sources, headers, compiler and flags differs
+from the stamp written beside it (``libfrei_hip.so.stamp``) — not by modification times, which a
+copied tree (the GPU box's snapshot) does not preserve meaningfully.  ``frei_amd._native``
+checks the same stamp at load time and refuses a library built from other sources.
+"""
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -8,23 +15,56 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = ["csrc/frei_kernels.hip", "csrc/frei_runtime.hip", "csrc/frei_binning.hip"]
 FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-shared", "-std=c++17"]
+LIB = os.path.join(HERE, "libfrei_hip.so")
+STAMP = LIB + ".stamp"
+
+
+def _hipcc():
+    return os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def source_files():
+    """Every file the library is built from (frei_math.h holds the sweep's division cores)."""
+    srcs = [os.path.join(HERE, s) for s in SOURCES]
+    return (srcs + sorted(glob.glob(os.path.join(HERE, "csrc", "*.h"))) +
+            sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
+
+
+def source_hash(extra_flags=()):
+    """SHA-256 over the sources' names and bytes and the build command's flags."""
+    h = hashlib.sha256()
+    for f in source_files():
+        h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    h.update(" ".join([*FLAGS, *extra_flags, "-ldl"]).encode())
+    return h.hexdigest()
+
+
+def stamp_matches(lib=LIB):
+    """True when ``lib`` exists and its stamp is the current sources' hash."""
+    try:
+        with open(lib + ".stamp") as f:
+            return os.path.exists(lib) and f.read().strip() == source_hash()
+    except OSError:
+        return False
 
 
 def build(verbose=False):
-    out = os.path.join(HERE, "libfrei_hip.so")
-    srcs = [os.path.join(HERE, s) for s in SOURCES]
-    # every header the sources include (frei_math.h holds the sweep's division/sqrt cores)
-    deps = (srcs + sorted(glob.glob(os.path.join(HERE, "csrc", "*.h"))) +
-            sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
-    if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
-        return out
-    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, *FLAGS, "-I" + os.path.join(ROOT, "include"), *srcs, "-o", out + ".tmp", "-ldl"]
+    if stamp_matches():
+        return LIB
+    digest = source_hash()
+    cmd = [_hipcc(), *FLAGS, "-I" + os.path.join(ROOT, "include"),
+           *[os.path.join(HERE, s) for s in SOURCES], "-o", LIB + ".tmp", "-ldl"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(out + ".tmp", out)
-    return out
+    os.replace(LIB + ".tmp", LIB)
+    with open(STAMP + ".tmp", "w") as f:
+        f.write(digest + "\n")
+    os.replace(STAMP + ".tmp", STAMP)
+    return LIB
 
 
 if __name__ == "__main__":

@@ -1421,8 +1421,7 @@ __device__ __forceinline__ void p2p_push_values(const P2PPush& p, int64_t idx, c
 
 // Wait until rank r's value idx of this sweep is published (flag == seq) or the timeout
 // passes (then *err = 1 and the value is used as is: the run is reported failed, not hung).
-__device__ __forceinline__ double p2p_take(const P2PWait& w, int r, int64_t idx,
-                                           long long t0) {
+__device__ __forceinline__ void p2p_wait(const P2PWait& w, int r, int64_t idx, long long t0) {
   const int par = (int)(w.seq & 1);
   const uint64_t* fl =
       reinterpret_cast<const uint64_t*>(w.mbox) + mbox_flag(par, r, w.nranks, w.n) + idx;
@@ -1435,8 +1434,19 @@ __device__ __forceinline__ double p2p_take(const P2PWait& w, int r, int64_t idx,
     }
     __builtin_amdgcn_s_sleep(1);
   }
-  // the mailbox is uncached and this load bypasses the caches: it is issued only after the
-  // flag load returned the new sequence number, behind the producer's release
+}
+
+// The acquire that pairs with p2p_push_values' system-scope release: issued after the flag
+// waits and before any p2p_value, so the value loads cannot be performed (by the compiler or
+// the memory system) ahead of the flag loads that observed this sweep's sequence number.
+__device__ __forceinline__ void p2p_acquire() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+// Rank r's value idx of this sweep (after p2p_wait + p2p_acquire); the mailbox is uncached
+// and the load is system-scope, so it reads memory.
+__device__ __forceinline__ double p2p_value(const P2PWait& w, int r, int64_t idx) {
+  const int par = (int)(w.seq & 1);
   const uint64_t* vp =
       reinterpret_cast<const uint64_t*>(w.mbox + mbox_val(par, r, w.nranks, w.n)) + idx;
   return __builtin_bit_cast(double,
@@ -1448,7 +1458,8 @@ __global__ void p2p_handshake_kernel(P2PPush push, P2PWait wait) {
   const double one = 1.0;
   p2p_push_values(push, 0, &one, 1);
   const long long t0 = wall_clock64();
-  for (int r = 0; r < wait.nranks; ++r) (void)p2p_take(wait, r, 0, t0);
+  for (int r = 0; r < wait.nranks; ++r) p2p_wait(wait, r, 0, t0);
+  p2p_acquire();
 }
 
 void launch_p2p_handshake(const P2PPush& push, const P2PWait& wait, hipStream_t st) {
@@ -1736,9 +1747,12 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
   for (int q = threadIdx.x; q < ntn; q += blockDim.x) sTn[q] = a.su.tnodes[q];
   if (a.p2p.mbox) {   // P2P: wait for every rank's sums of this sweep, add in rank order
     const long long t0 = wall_clock64();
+    for (int q = threadIdx.x; q < ns * 4; q += blockDim.x)
+      for (int r = 0; r < a.p2p.nranks; ++r) p2p_wait(a.p2p, r, q, t0);
+    p2p_acquire();
     for (int q = threadIdx.x; q < ns * 4; q += blockDim.x) {
-      double v = p2p_take(a.p2p, 0, q, t0);
-      for (int r = 1; r < a.p2p.nranks; ++r) v += p2p_take(a.p2p, r, q, t0);
+      double v = p2p_value(a.p2p, 0, q);
+      for (int r = 1; r < a.p2p.nranks; ++r) v += p2p_value(a.p2p, r, q);
       sFb[q] = v;
     }
     __syncthreads();
@@ -1941,9 +1955,12 @@ __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a)
       v = tot[tid];
       if (a.p2p.mbox) {
         const double own = v;
+        const int64_t idx = (int64_t)k * 4 + (tid & 3);
+        for (int r = 0; r < a.p2p.nranks; ++r)
+          if (r != a.push.rank) p2p_wait(a.p2p, r, idx, t0);
+        p2p_acquire();
         for (int r = 0; r < a.p2p.nranks; ++r) {
-          const double x =
-              (r == a.push.rank) ? own : p2p_take(a.p2p, r, (int64_t)k * 4 + (tid & 3), t0);
+          const double x = (r == a.push.rank) ? own : p2p_value(a.p2p, r, idx);
           v = (r == 0) ? x : v + x;
         }
       }

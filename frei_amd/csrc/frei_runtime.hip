@@ -1401,7 +1401,11 @@ static int iterate(frei_ctx* c, int n, int nzc, double thr, double alpha, bool s
   std::vector<uint64_t> key;
   c->keys = &key;
   c->dry = true;
+  // the dry pass launches nothing, so it must leave no state behind that a real sweep reads:
+  // run_sweep clears / sets rec_skipped as it would for real launches
+  const bool rec_skipped = c->rec_skipped;
   const int rc = iterate_direct(c, 1, nzc, thr, alpha, stop);
+  c->rec_skipped = rec_skipped;
   c->dry = false;
   c->keys = nullptr;
   TRY(rc);

@@ -16,7 +16,7 @@ from . import _native as N
 from .binning import BinnedTable
 from .chemistry import ChemistryTable, chemistry
 from .constants import BAR, C, H, K_B, M_BAR_DEFAULT, UM
-from .opacity import SeparableTable, sigma_scattering
+from .opacity import SeparableTable, sigma_scattering, table_values
 from .units import scalar, value
 
 EMIT, ABSORB = 0, 1
@@ -178,7 +178,7 @@ class Engine:
                 self._ctx, s, N.dptr(N.f64(tab.base[sl])), N.dptr(N.f64(tab.fp)),
                 N.dptr(N.f64(tab.fT)), tab.lo, tab.hi, N.dptr(p_cgs), p.size, N.dptr(T), T.size))
             return
-        vals = np.asarray(tab.values)
+        vals = table_values(tab)      # transposed by name when the table carries .dims
         if vals.ndim != 3 or vals.shape[:2] != (p.size, T.size):
             raise ValueError("opacity table must be (pressure, temperature, wavelength)")
         if vals.shape[2] != self.lam_um.size:
@@ -332,7 +332,8 @@ class Engine:
 # contexts, keyed on the identity of the opacity dict and its tables plus the grid arrays.
 # Tables are treated as immutable while cached: after editing table values in place, call
 # clear_engine_cache().
-_ENGINE_CACHE = []       # [(key, opacities (kept alive so its id stays unique), engine)]
+# [(key, (opacities, its tables) — kept alive so their ids stay unique while cached, engine)]
+_ENGINE_CACHE = []
 _ENGINE_CACHE_SIZE = 2
 
 
@@ -362,7 +363,7 @@ def cached_engine(opacities, *, lam_um, p_bar, g, m_bar, F_toa, mmr=None, device
             return eng
     eng = Engine(lam_um, p_bar, opacities, g=g, m_bar=m_bar, F_toa=F_toa, mmr=mmr,
                  device=device)
-    _ENGINE_CACHE.insert(0, (key, opacities, eng))
+    _ENGINE_CACHE.insert(0, (key, (opacities, tuple(opacities.values())), eng))
     while len(_ENGINE_CACHE) > _ENGINE_CACHE_SIZE:
         _ENGINE_CACHE.pop()[2].close()
     return eng

@@ -17,13 +17,53 @@ N_REF_H2 = 2.68678e19   # cm^-3, opacity.py:23
 N_REF_HE = 2.546899e19  # cm^-3, opacity.py:24
 
 
+TABLE_DIMS = ("pressure", "temperature", "wavelength")
+
+
+def table_values(tab):
+    """A table's values as (pressure, temperature, wavelength).
+
+    The reference's tables are xarray DataArrays whose axes are found by NAME — ``kappa``
+    interpolates ``pressure=`` / ``temperature=`` (opacity.py:252-263) — and the three
+    producers lay them out differently: ``load_example_opacity`` (pressure, temperature,
+    wavelength) (opacity.py:338-342), ``binned_opacity(groupies=True)`` (temperature,
+    pressure, wavelength) (interp.py:287-307, opacity.py:137-146) and the default
+    ``binned_opacity(groupies=False)`` of ``Grid.load_opacities`` (wavelength, temperature,
+    pressure) (opacity.py:42, 156-167).  A table carrying ``.dims`` is therefore transposed by
+    name; one without ``.dims`` (a plain object with ``.values``) must already be (pressure,
+    temperature, wavelength).  Dims other than those three names raise ValueError: on a Grid
+    n_T = n_p, so a positional guess could silently swap p and T."""
+    vals = np.asarray(tab.values)
+    dims = getattr(tab, "dims", None)
+    if dims is None:
+        return vals
+    dims = tuple(str(d) for d in dims)
+    if len(dims) != vals.ndim or sorted(dims) != sorted(TABLE_DIMS):
+        raise ValueError(f"opacity table dims {dims} are not a permutation of {TABLE_DIMS}")
+    return np.transpose(vals, [dims.index(d) for d in TABLE_DIMS])
+
+
 class OpacityTable:
-    """(pressure, temperature, wavelength) opacity grid in cm^2 g^-1."""
+    """(pressure, temperature, wavelength) opacity grid in cm^2 g^-1.
 
-    dims = ("pressure", "temperature", "wavelength")
+    ``dims`` names the axes of ``values`` when they come in another order (e.g. a reference
+    DataArray's ``.dims``); the values are stored transposed to (pressure, temperature,
+    wavelength).  :meth:`from_dataarray` takes any object with ``.values``, ``.dims``,
+    ``.pressure`` (bar), ``.temperature`` (K) and optionally ``.wavelength`` (µm)."""
 
-    def __init__(self, values, pressure, temperature, wavelength=None):
-        self.values = np.asarray(values, dtype=np.float64)
+    dims = TABLE_DIMS
+
+    @classmethod
+    def from_dataarray(cls, da):
+        wl = getattr(da, "wavelength", None)
+        return cls(table_values(da), np.asarray(da.pressure), np.asarray(da.temperature),
+                   None if wl is None else np.asarray(wl))
+
+    def __init__(self, values, pressure, temperature, wavelength=None, dims=None):
+        values = np.asarray(values, dtype=np.float64)
+        if dims is not None:
+            values = table_values(_Dimmed(values, dims))
+        self.values = values
         self.pressure = np.asarray(value(pressure, "bar"), dtype=np.float64)
         self.temperature = np.asarray(value(temperature, "K"), dtype=np.float64)
         self.wavelength = None if wavelength is None else np.asarray(value(wavelength, "um"))
@@ -42,6 +82,11 @@ class OpacityTable:
         idx = np.sort(idx)
         return OpacityTable(self.values[:, idx], self.pressure, self.temperature[idx],
                             self.wavelength)
+
+
+class _Dimmed:
+    def __init__(self, values, dims):
+        self.values, self.dims = values, dims
 
 
 class SeparableTable:

@@ -43,6 +43,16 @@ def _recv(sock):
     return _recv_exact(sock, n)
 
 
+def _read_port(path):
+    """("127.0.0.1", port) from rank 0's port file, or None while it is absent / half written."""
+    try:
+        with open(path) as f:
+            txt = f.read().strip()
+        return ("127.0.0.1", int(txt)) if txt else None
+    except (OSError, ValueError):
+        return None
+
+
 class Rendezvous:
     """``world`` ranks, this one ``rank``; see the module docstring for discovery."""
 
@@ -85,19 +95,20 @@ class Rendezvous:
                         pass
             self._peers = [by_rank[r] for r in range(1, self.world)]
         else:
-            if addr is None:
-                path = _port_file(tag)
-                while not os.path.exists(path):
-                    if time.monotonic() > deadline:
-                        raise TimeoutError(f"rendezvous: rank 0 never published {path}")
-                    time.sleep(0.01)
-                addr = ("127.0.0.1", int(open(path).read()))
+            path = _port_file(tag) if addr is None else None
             while True:
+                # the port file is re-read before every attempt: a stale file left by a crashed
+                # earlier launch with the same key is replaced when rank 0 publishes its port
+                target = addr if path is None else _read_port(path)
                 try:
-                    s = socket.create_connection(addr, timeout=5.0)
+                    if target is None:
+                        raise OSError("port not published yet")
+                    s = socket.create_connection(target, timeout=5.0)
                     break
                 except OSError:
                     if time.monotonic() > deadline:
+                        if target is None:
+                            raise TimeoutError(f"rendezvous: rank 0 never published {path}")
                         raise
                     time.sleep(0.05)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)

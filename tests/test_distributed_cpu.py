@@ -124,3 +124,33 @@ def test_pointwise_trapz_weights_equal_np_trapz():
     # slices sum to the whole without a halo
     parts = [np.sum(w[a:b] * f[a:b]) for a, b in (partition(lam.size, 4, r) for r in range(4))]
     assert abs(sum(parts) - ref) / ref < 1e-14
+
+
+def test_sharded_oracle_matches_one_process_oracle():
+    """tests/sharded_oracle.py (the checker of the full-size GPU parity tests) against the
+    one-process oracle: same iterations, T within 1e-12, spectrum and fluxes within 1e-10."""
+    from tests.parity import rel, row_normwise
+    from tests.sharded_oracle import ShardedOracle
+    rng = np.random.default_rng(8)
+    lam, _, _ = O.wavelength_grid(0.5, 10, 1501)
+    p = O.pressure_grid(16, -6, np.log10(200))
+    T0 = O.temperature_grid(p, 1800.0, 0.1, 0.1)
+    Tn = T0.copy()                                   # descending nodes, n_T = n_p
+    names = ["1H2-16O", "12C-16O", "Na"]
+    mmr = O.mock_mmr(names, M_BAR)[:, None] * np.ones(p.size)
+    spec = {n: (10 ** rng.uniform(-3, 2, lam.size), (p / 1.0) ** 0.1, (Tn / 1000) ** 0.5, Tn)
+            for n in names}
+    tabs = {n: O.Table(O.separable_table(b, fp, fT), p, t) for n, (b, fp, fT, t) in spec.items()}
+    Ft = O.F_TOA(lam)
+    ref = O.emission_spectrum(tabs, T0, p, lam, Ft, G_J, M_BAR, 1, n_timesteps=4, mmr=mmr)
+    with ShardedOracle(spec, lam, p, T0, Ft, G_J, M_BAR, mmr=mmr, n_workers=3) as so:
+        got = so.emission_spectrum(n_timesteps=4)
+        got2 = so.emission_spectrum(n_timesteps=4)       # workers are reusable
+        pert = so.emission_spectrum(perturb=True, n_timesteps=4)
+    assert got[6] == ref[6]
+    assert rel(got[1], ref[1]) < 1e-12
+    assert rel(got[0], ref[0]) < 1e-10
+    assert row_normwise(got[4], ref[4]) < 1e-10 and row_normwise(got[5], ref[5]) < 1e-10
+    assert row_normwise(got[3], ref[3]) < 1e-12
+    assert all(np.array_equal(a, b) for a, b in zip(got[:6], got2[:6]))
+    assert not np.array_equal(pert[0], got[0])        # the perturbation reached the workers

@@ -71,7 +71,7 @@ def test_batched_atmospheres_match_oracle_per_atmosphere(fa):
                 convergence_dT=3.0, mmr=mmr[m])
         floor = grid_floor(osp, ou, od, psp, pu, pd)
         assert_grid_parity(out["spectra"][m], osp, ups[m], ou, downs[m], od, f"atmosphere {m}",
-                           floor)
+                           floor, T=out["final_T"][m], ref_T=oT)
 
 
 def test_batched_mfma_contraction_tiles_and_padding(fa):

@@ -140,3 +140,29 @@ def test_graph_replay_is_bitwise_identical_to_launches(fa, name, opts):
             _same(a[key][what], b[key][what], f"{name} {key} {what}")
     _same(a["run"]["final_T"], a["run_again"]["final_T"], "graph reuse")
     _same(a["iterate"], b["iterate"], f"{name} iterate T")
+
+
+def test_graph_key_pass_keeps_record_state_when_rec_sweep_changes(fa):
+    """The graph key pass (a dry iteration that only hashes launch arguments) must not clear the
+    'last update wrote no step records' flag: with records formed in the sweep, then turned off
+    between two frei_iterate calls, the first real sweep must write its own records first — the
+    graph path gives bitwise the direct path's temperatures."""
+    lam, p, T0, tabs, mmr = _case(fa, "contracted")
+    out = {}
+    for graph in (1, 0):
+        eng = fa.Engine(lam, p, tabs, mmr=mmr)
+        try:
+            eng.set_option("graph", graph)
+            eng.set_option("rec_sweep", 1)
+            eng.state_init(T0)
+            eng.iterate(5, n_zero_crossings=10 ** 6, convergence_dT=-1.0)
+            eng.set_option("rec_sweep", 0)
+            eng.iterate(5, n_zero_crossings=10 ** 6, convergence_dT=-1.0)
+            eng.synchronize()
+            out[graph] = eng.get_temperatures()
+            if graph:
+                cap, rep = eng.graph_info()
+                assert cap >= 1 and rep >= 1, (cap, rep)
+        finally:
+            eng.close()
+    _same(out[1], out[0], "graph vs direct after a rec_sweep change")
