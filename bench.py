@@ -229,6 +229,8 @@ def c5_leg(a, d):
         eng.state_init(T0)       # metadata + K7 contraction (fp64 MFMA), once
         eng.synchronize()
         setup_s = time.perf_counter() - t_s
+        k7 = eng.contract_timing()
+        phases = eng.setup_timing()
         eng.iterate(1)
         eng.synchronize()
         d.barrier()
@@ -261,6 +263,16 @@ def c5_leg(a, d):
                        "note": "iterations per atmosphere under the reference's convergence "
                                "test; an atmosphere at max_iterations did not meet it"},
             "setup_s": setup_s,
+            "setup_phases_ms": phases,
+            "k7_roofline": {"bound": "hbm", "kernel": "contract_batch_kernel",
+                            "avg_launch_ms": k7["ms"], "bytes_per_launch": k7["bytes"],
+                            "achieved": k7["bytes"] / (k7["ms"] * 1e-3) / 1e9,
+                            "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                            "frac": k7["bytes"] / (k7["ms"] * 1e-3) / PEAK_HBM,
+                            "byte_model": "the S tables' used pressure rows read once + one "
+                                          "contracted table per atmosphere written (n_T x "
+                                          "pitch columns per used row), one launch per "
+                                          "tables/mmr; HIP events on the engine stream"},
             "note": "setup_s: table generation + metadata + K7 MFMA contraction, once"}
 
 

@@ -72,6 +72,7 @@ SIGNATURES = {
     "frei_contribution": (ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, ctypes.c_double, _dp]),
     "frei_set_option": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int]),
     "frei_setup_timing": (ctypes.c_int, [_vp, _dp]),
+    "frei_contract_timing": (ctypes.c_int, [_vp, _dp, _dp]),
     "frei_graph_info": (ctypes.c_int, [_vp, _ip, _ip]),
     "frei_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "frei_timing_read": (ctypes.c_int, [_vp, _dp, _ip]),

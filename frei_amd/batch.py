@@ -117,6 +117,12 @@ class BatchEngine:
         N.check(N.lib().frei_timing_read(self._ctx, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def setup_timing(self):
+        return Engine.setup_timing(self)
+
+    def contract_timing(self):
+        return Engine.contract_timing(self)
+
     def get_fluxes(self):
         up = np.empty((self.n_atm, self.n_layers, self.n_lam))
         down = np.empty_like(up)

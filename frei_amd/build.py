@@ -55,12 +55,27 @@ def build(verbose=False):
     if stamp_matches():
         return LIB
     digest = source_hash()
-    cmd = [_hipcc(), *FLAGS, "-I" + os.path.join(ROOT, "include"),
-           *[os.path.join(HERE, s) for s in SOURCES], "-o", LIB + ".tmp", "-ldl"]
+    # one object per translation unit, compiled in parallel (no relocatable device code: every
+    # kernel is launched from its own unit), then linked
+    compile_flags = [f for f in FLAGS if f != "-shared"]
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = os.path.join(HERE, "build_" + os.path.basename(src).replace(".hip", ".o"))
+        cmd = [_hipcc(), *compile_flags, "-I" + os.path.join(ROOT, "include"), "-c",
+               os.path.join(HERE, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    if any(p.wait() != 0 for p in procs):
+        raise subprocess.CalledProcessError(1, "hipcc")
+    cmd = [_hipcc(), *FLAGS, *objs, "-o", LIB + ".tmp", "-ldl"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
+    for o in objs:
+        os.unlink(o)
     with open(STAMP + ".tmp", "w") as f:
         f.write(digest + "\n")
     os.replace(STAMP + ".tmp", STAMP)

@@ -360,7 +360,7 @@ __host__ __device__ inline size_t update_lds_bytes(int nL, int ntn, int S, bool 
 
 // launchers (frei_kernels.hip)
 void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st);
-void launch_sweep_fast(int dir, int S, int depth, bool nan_check, bool shared,
+void launch_sweep_fast(int dir, int S, int depth, int pf, bool nan_check, bool shared,
                        const FastArgs& a, int nblocks, hipStream_t st);
 // Grouped-lane sweep (Q = 2 or 4 lanes per wavelength, 256/Q wavelengths per block):
 // contracted single table, step table in LDS; for slices with about one wave per SIMD.

@@ -524,12 +524,17 @@ __device__ __forceinline__ void stage_records(const FastArgs& a, int dir, FastSt
   __syncthreads();
 }
 
-template <int DIR, int S, int PD, bool NANCHK, bool SH, bool MM1>
+// PD steps form one coefficient block; PF (a multiple of PD) is the prefetch distance: the
+// loads of step k + PF are issued while step k computes, into a register ring of PF entries
+// (the step loop is unrolled by PF, so every ring index is static).  PF > PD pays on small
+// slices, where about one wave per SIMD cannot hide HBM latency with PD steps of loads alone.
+template <int DIR, int S, int PD, bool NANCHK, bool SH, bool MM1, int PF>
 __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     FastArgs a, const FastStep* __restrict__ st, const FastStepS* __restrict__ ss,
     double* __restrict__ Fu, double* __restrict__ Fd, double* __restrict__ part,
     double* __restrict__ dtaus) {
   static_assert(PD == 1 || PD == 2 || PD == 4, "prefetch depth 1, 2 or 4");
+  static_assert(PF % PD == 0, "prefetch distance: a multiple of the coefficient block");
   static_assert(!MM1 || S == 1, "mmr = 1 only for the contracted single table");
   {  // atmosphere of a batched launch (identity for one atmosphere)
     const int m = blockIdx.y;
@@ -657,7 +662,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       tot = (s == 0) ? ops : tot + ops;
     }
     c.F_st = stale;
-    load(k + PD, v, stale);
+    load(k + PF, v, stale);
     const double kap = tot + sig;
     const double dtau = dm * kap;
     const double w0 = fm::div(sig, sig + kap);
@@ -755,16 +760,20 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   }
   // PD steps in flight: their loads are issued PD steps ahead, their coefficients form one
   // block (PD-way instruction-level parallelism), then the short carried recurrence.
-  double vb[PD][2 * S], sb[PD];
+  double vb[PF][2 * S], sb[PF];
 #pragma unroll
-  for (int b = 0; b < PD; ++b) load(b, vb[b], sb[b]);
-  for (int k = 0; k < ns; k += PD) {
+  for (int b = 0; b < PF; ++b) load(b, vb[b], sb[b]);
+  for (int k0 = 0; k0 < ns; k0 += PF) {
+#pragma unroll
+  for (int g = 0; g < PF / PD; ++g) {
+    const int k = k0 + g * PD;
+    if (PF > PD && k >= ns) break;   // wave-uniform: no dummy coefficient blocks at the end
     StepCoef c[PD];
     PreCoef pc[PD];
     double Bp = Bc;
 #pragma unroll
     for (int b = 0; b < PD; ++b) {
-      coef(k + b, vb[b], sb[b], Bp, c[b], pc[b]);
+      coef(k + b, vb[g * PD + b], sb[g * PD + b], Bp, c[b], pc[b]);
       Bp = c[b].Bnext;
     }
     Bc = Bp;
@@ -789,6 +798,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
         __builtin_amdgcn_wave_barrier();
       }
     }
+  }
   }
   __syncthreads();
   for (int idx = tid; idx < ns * 4; idx += kBlock) {
@@ -2228,8 +2238,14 @@ void launch_contribution(const double* dtaus, int nL, int64_t n, const double* n
 //   eff[m][prow_l][c] = sum_s mmr[m][s][l] * tab_s[prow_l][c],
 // i.e. per layer the dense product [n_atm x S] . [S x n_T*pitch].  v_mfma_f64_16x16x4f64:
 // A = 16 atmospheres x 4 species (mixing ratios), B = 4 species x 16 columns (table values),
-// D = 16 atmospheres x 16 columns; K = S in steps of 4.  Each wave owns 16 columns for all
-// atmosphere tiles, so every table value is read once from HBM.
+// D = 16 atmospheres x 16 columns; K = S in steps of 4.  Each wave owns 64 columns (four
+// column tiles) for all atmosphere tiles, so every table value is read once from HBM.
+//
+// The stores are the traffic (n_atm contracted tables against one read of the S tables), so
+// they are shaped for HBM: a D tile leaves each lane 4 atmospheres x 1 column, i.e. 4-row x
+// 128-B pieces per store instruction; instead each wave parks its 16 x 64 D block in LDS
+// (rows padded to 80 doubles: the two lane halves of a ds_write_b64 hit disjoint banks) and
+// stores it back row by row, one atmosphere's 64 contiguous columns (512 B) per instruction.
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 struct ContractBatchArgs {
@@ -2241,39 +2257,104 @@ struct ContractBatchArgs {
   int64_t pitch, tab_stride;
 };
 
+#ifndef FREI_K7_WIDE
+#define FREI_K7_WIDE 1
+#endif
+#ifndef FREI_K7_NT
+#define FREI_K7_NT 0
+#endif
+#if FREI_K7_WIDE
+// 128 columns per wave, 16 B per lane per store: each store instruction writes one
+// atmosphere's 128 contiguous columns (1 KiB); the 16 x 128 D block goes through LDS in two
+// halves of 8 atmospheres (rows padded to 144 doubles: 1152 B = 128 B mod 256)
+constexpr int kK7Cols = 128;
+constexpr int kK7Row = kK7Cols + 16;
+constexpr int kK7Rows = 8;
+#else
+constexpr int kK7Cols = 64;          // columns per wave (four 16-column MFMA tiles)
+constexpr int kK7Row = kK7Cols + 16; // LDS row pitch in doubles (640 B: 128 B mod 256)
+constexpr int kK7Rows = 16;
+#endif
+constexpr int kK7Tiles = kK7Cols / 16;
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void k7_store(double* p, double v) {
+#if FREI_K7_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ void k7_store(dbl2* p, dbl2 v) {
+#if FREI_K7_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 __global__ __launch_bounds__(256) void contract_batch_kernel(ContractBatchArgs a) {
+  __shared__ double tile[4][kK7Rows * kK7Row];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l = blockIdx.y;
-  const int64_t ncol = (int64_t)a.n_T * a.pitch;
-  const int64_t col0 = ((int64_t)blockIdx.x * 4 + wv) * 16;
-  if (col0 >= ncol) return;
+  const int64_t ncol = (int64_t)a.n_T * a.pitch;   // a multiple of 64 (pitch is)
+  const int64_t col0 = ((int64_t)blockIdx.x * 4 + wv) * kK7Cols;
   const int64_t rowbase = (int64_t)a.prow[l] * ncol;
   const int ci = lane & 15, kq = lane >> 4;   // column in the tile, species in the K step
-  const int64_t col = col0 + ci;
-  const bool colok = col < ncol;
   constexpr int kSteps = kMaxFastS / 4;
-  double b[kSteps];
+  double b[kK7Tiles][kSteps];
 #pragma unroll
-  for (int ks = 0; ks < kSteps; ++ks) {
-    const int s = 4 * ks + kq;
-    b[ks] = (s < a.S && colok) ? a.tab[s][rowbase + col] : 0.0;
-  }
-  for (int m0 = 0; m0 < a.n_atm; m0 += 16) {
-    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-    const int am = m0 + ci;                     // A operand row: atmosphere
+  for (int t = 0; t < kK7Tiles; ++t)
 #pragma unroll
     for (int ks = 0; ks < kSteps; ++ks) {
-      if (4 * ks >= a.S) break;
       const int s = 4 * ks + kq;
-      const double av =
-          (am < a.n_atm && s < a.S) ? a.mmr[((int64_t)am * a.S + s) * a.n_layers + l] : 0.0;
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b[ks], acc, 0, 0, 0);
+      const int64_t c = col0 + 16 * t + ci;
+      b[t][ks] = (s < a.S && c < ncol) ? a.tab[s][rowbase + c] : 0.0;
     }
-    // D: this lane holds rows kq + 4 r (atmospheres) of column ci
+  double* my = tile[wv];
+  for (int m0 = 0; m0 < a.n_atm; m0 += 16) {
+    const int am = m0 + ci;                     // A operand row: atmosphere
+    double av[kSteps];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + kq + 4 * r;
-      if (m < a.n_atm && colok) a.eff[(int64_t)m * a.tab_stride + rowbase + col] = acc[r];
+    for (int ks = 0; ks < kSteps; ++ks) {
+      const int s = 4 * ks + kq;
+      av[ks] = (am < a.n_atm && s < a.S) ? a.mmr[((int64_t)am * a.S + s) * a.n_layers + l]
+                                         : 0.0;
+    }
+    dbl4 acc[kK7Tiles];
+#pragma unroll
+    for (int t = 0; t < kK7Tiles; ++t) {
+      acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int ks = 0; ks < kSteps; ++ks) {
+        if (4 * ks >= a.S) break;
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b[t][ks], acc[t], 0, 0, 0);
+      }
+    }
+    // D: this lane holds rows kq + 4 r (atmospheres) of column 16 t + ci
+#pragma unroll
+    for (int h = 0; h < 16 / kK7Rows; ++h) {
+#pragma unroll
+      for (int t = 0; t < kK7Tiles; ++t)
+#pragma unroll
+        for (int rr = 0; rr < kK7Rows / 4; ++rr)
+          my[(kq + 4 * rr) * kK7Row + 16 * t + ci] = acc[t][h * (kK7Rows / 4) + rr];
+      __syncthreads();
+      const int mlo = m0 + h * kK7Rows;
+      const int mrows = max(0, min(kK7Rows, a.n_atm - mlo));
+#if FREI_K7_WIDE
+      if (col0 + 2 * lane < ncol)
+        for (int m = 0; m < mrows; ++m)
+          k7_store(reinterpret_cast<dbl2*>(a.eff + (int64_t)(mlo + m) * a.tab_stride + rowbase +
+                                           col0 + 2 * lane),
+                   *reinterpret_cast<const dbl2*>(my + m * kK7Row + 2 * lane));
+#else
+      if (col0 < ncol)
+        for (int m = 0; m < mrows; ++m)
+          k7_store(a.eff + (int64_t)(mlo + m) * a.tab_stride + rowbase + col0 + lane,
+                   my[m * kK7Row + lane]);
+#endif
+      __syncthreads();   // the next half / atmosphere tile overwrites this wave's LDS block
     }
   }
 }
@@ -2293,7 +2374,7 @@ void launch_contract_batch(const double* const* tabs, int S, const double* mmr,
   a.pitch = pitch;
   a.tab_stride = tab_stride;
   const int64_t ncol = (int64_t)n_T * pitch;
-  dim3 grid((unsigned)((ncol + 63) / 64), (unsigned)n_layers);
+  dim3 grid((unsigned)((ncol + 4 * kK7Cols - 1) / (4 * kK7Cols)), (unsigned)n_layers);
   hipLaunchKernelGGL(contract_batch_kernel, grid, dim3(256), 0, st, a);
 }
 
@@ -2320,15 +2401,23 @@ void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream
   else launch_sweep_dir<kAbsorb>(a, nblocks, fast, st);
 }
 
-template <int DIR, int S, int PD, bool NC, bool SH, bool MM1 = false>
+template <int DIR, int S, int PD, bool NC, bool SH, bool MM1 = false, int PF = PD>
 static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
   const size_t shm = (size_t)red_lds_doubles(a.red_rows, a.n_steps) * sizeof(double) +
                      (SH ? (size_t)a.n_steps * sizeof(FastStepS) +
                                (size_t)rec_scratch_doubles(a) * sizeof(double)
                          : 0);
-  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC, SH, MM1>),
+  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC, SH, MM1, PF>),
                      dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1), dim3(kBlock), shm,
                      st, a, a.steps, a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+}
+
+// the contracted one-table sweep (S = 1, unit mmr) with prefetch distance pf (0: = PD)
+template <int DIR, int PD, bool SH>
+static void launch_fast_pf(int pf, const FastArgs& a, int nblocks, hipStream_t st) {
+  if (pf >= 16) return launch_fast_t<DIR, 1, PD, false, SH, true, 16>(a, nblocks, st);
+  if (pf >= 8) return launch_fast_t<DIR, 1, PD, false, SH, true, 8>(a, nblocks, st);
+  return launch_fast_t<DIR, 1, PD, false, SH, true, PD>(a, nblocks, st);
 }
 
 template <int DIR, int PD, bool NC, bool SH>
@@ -2354,8 +2443,19 @@ static void launch_fast_pd(int dir, int S, const FastArgs& a, int nblocks, hipSt
 }
 
 template <bool SH>
-static void launch_fast_sh(int dir, int S, int depth, bool nan_check, const FastArgs& a,
+static void launch_fast_sh(int dir, int S, int depth, int pf, bool nan_check, const FastArgs& a,
                            int nblocks, hipStream_t st) {
+  if (pf > depth && S == 1 && a.unit_mmr && !nan_check && depth >= 2) {
+    // the contracted table with loads issued pf steps ahead
+    if (depth >= 4) {
+      if (dir == kEmit) launch_fast_pf<kEmit, 4, SH>(pf, a, nblocks, st);
+      else launch_fast_pf<kAbsorb, 4, SH>(pf, a, nblocks, st);
+    } else {
+      if (dir == kEmit) launch_fast_pf<kEmit, 2, SH>(pf, a, nblocks, st);
+      else launch_fast_pf<kAbsorb, 2, SH>(pf, a, nblocks, st);
+    }
+    return;
+  }
   if (depth >= 4 && S == 1 && !nan_check) {  // 4 steps in flight: small slices, one table
     if (a.unit_mmr) {
       if (dir == kEmit) launch_fast_t<kEmit, 1, 4, false, SH, true>(a, nblocks, st);
@@ -2373,10 +2473,10 @@ static void launch_fast_sh(int dir, int S, int depth, bool nan_check, const Fast
   }
 }
 
-void launch_sweep_fast(int dir, int S, int depth, bool nan_check, bool shared,
+void launch_sweep_fast(int dir, int S, int depth, int pf, bool nan_check, bool shared,
                        const FastArgs& a, int nblocks, hipStream_t st) {
-  if (shared) launch_fast_sh<true>(dir, S, depth, nan_check, a, nblocks, st);
-  else launch_fast_sh<false>(dir, S, depth, nan_check, a, nblocks, st);
+  if (shared) launch_fast_sh<true>(dir, S, depth, pf, nan_check, a, nblocks, st);
+  else launch_fast_sh<false>(dir, S, depth, pf, nan_check, a, nblocks, st);
 }
 
 __global__ void nan_scan_kernel(const double* __restrict__ x, int64_t n, int* flag) {

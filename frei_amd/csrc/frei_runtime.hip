@@ -176,6 +176,8 @@ struct frei_ctx {
   void* comm = nullptr;
   int nranks = 1, rank = 0;
   int prefetch_depth = 0;               // 0 = automatic (FREI_PREFETCH_DEPTH overrides)
+  int prefetch_steps = 0;               // FREI_PREFETCH_STEPS: contracted one-lane sweep's load
+                                        // distance in steps (0 = automatic, 8 / 16 = deeper)
   // Shared-bracket kernel (step table staged in LDS): used when every species shares its
   // nodes AND the slice is small (nblocks <= shared_max_blocks, about one resident round of
   // blocks), where each CU runs ~1 block and the per-step scalar loads would miss the K$.
@@ -206,6 +208,8 @@ struct frei_ctx {
   size_t lds_optin = 64 * 1024;         // with the dynamic-LDS opt-in (gfx950: 160 KiB)
   bool ftoa_per_atm = false;            // batched: one F_TOA per atmosphere (frei_set_ftoa_batch)
   double setup_ms[5] = {0, 0, 0, 0, 0};  // last metadata build, by phase (frei_setup_timing)
+  double contract_ms = 0.0;     // last K3 / K7 kernel, HIP events (frei_contract_timing)
+  double contract_bytes = 0.0;  // its algorithmic HBM bytes
   // T-dependent chemistry (frei_set_chemistry): mmr tables on (T, p) nodes
   bool chem_on = false;
   int chem_nT = 0, chem_np = 0;
@@ -313,7 +317,30 @@ int build_contracted(frei_ctx* c, bool shared_fast, Lap&& lap) {
   }
   lap(2);
   c->eff_stride = per;
-  HIP_TRY(hipMemsetAsync(c->d_eff, 0, need * sizeof(double), c->stream));
+  // the contraction writes every column (padding included) of the pressure rows the layers
+  // use; only the other rows and each atmosphere's 64-element tail are zero-filled here (a
+  // fill of the whole table would double the setup's HBM writes: 24.6 GB at C5)
+  {
+    const size_t rowblk = (size_t)q0.n_T * q0.stride;
+    std::vector<char> used((size_t)q0.n_p, 0);
+    for (int l = 0; l < nL; ++l) used[prow[l]] = 1;
+    for (size_t m = 0; m < (size_t)c->n_atm; ++m) {
+      double* base = c->d_eff + m * per;
+      for (int p = 0; p < q0.n_p;) {
+        if (used[p]) {
+          ++p;
+          continue;
+        }
+        int e = p;
+        while (e < q0.n_p && !used[e]) ++e;
+        HIP_TRY(hipMemsetAsync(base + (size_t)p * rowblk, 0,
+                               (size_t)(e - p) * rowblk * sizeof(double), c->stream));
+        p = e;
+      }
+      HIP_TRY(hipMemsetAsync(base + (size_t)q0.n_p * rowblk, 0, 64 * sizeof(double),
+                             c->stream));
+    }
+  }
   lap(3);
   if (!c->d_ones) {
     std::vector<double> ones(nL, 1.0);
@@ -325,13 +352,34 @@ int build_contracted(frei_ctx* c, bool shared_fast, Lap&& lap) {
   TRY(h2d(c->d_prow, prow.data(), nL, c->stream));
   const double* tabs[kMaxFastS];
   for (int s = 0; s < S; ++s) tabs[s] = c->sp[s].d_tab;
+  hipEvent_t k0 = nullptr, k1 = nullptr;   // the contraction kernel alone (frei_contract_timing)
+  if (hipEventCreate(&k0) != hipSuccess || hipEventCreate(&k1) != hipSuccess)
+    return fail("hipEventCreate failed");
+  HIP_TRY(hipEventRecord(k0, c->stream));
   if (batch)  // K7: [n_atm x S] . [S x n_T*pitch] per layer on fp64 MFMA
     launch_contract_batch(tabs, S, c->d_mmr, c->d_prow, nL, q0.n_T, q0.stride, c->n_atm,
                           (int64_t)per, c->d_eff, c->stream);
   else
     launch_contract(tabs, S, c->d_mmr, c->d_prow, nL, q0.n_T, q0.stride, c->d_eff, c->stream);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(k1, c->stream));
   lap(4);
+  {
+    float ms = 0.f;
+    HIP_TRY(hipEventSynchronize(k1));
+    HIP_TRY(hipEventElapsedTime(&ms, k0, k1));
+    c->contract_ms = ms;
+    // bytes the launch must move: the S tables' used rows read once, n_atm tables written
+    // (every column of the used rows, padding included)
+    std::vector<char> used((size_t)q0.n_p, 0);
+    for (int l = 0; l < nL; ++l) used[prow[l]] = 1;
+    size_t rows = 0;
+    for (char u : used) rows += u;
+    const double rowbytes = (double)q0.n_T * q0.stride * sizeof(double);
+    c->contract_bytes = rows * rowbytes * (S + c->n_atm);
+    (void)hipEventDestroy(k0);
+    (void)hipEventDestroy(k1);
+  }
   SpecMeta m = c->smeta[0];
   m.tab = c->d_eff;
   if (!c->d_smeta_eff) TRY(dalloc(&c->d_smeta_eff, 1));
@@ -643,6 +691,8 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     // instruction-level parallelism that occupancy cannot (FREI_DEPTH4_MAX_BLOCKS).
     const int depth = c->prefetch_depth > 0 ? c->prefetch_depth
                       : (S_run == 1 && c->nblocks <= c->depth4_max_blocks) ? 4 : 2;
+    // loads issued pf steps ahead (the contracted table only; 0: the coefficient block's depth)
+    const int pf = (c->eff && S_run == 1 && depth >= 2) ? c->prefetch_steps : 0;
     bool nan_check = false;
     for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
     const int Q = group_lanes(c);
@@ -657,8 +707,8 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     if (NC > 0) nb_run = (int)((c->nlam + 64 * NC - 1) / (64 * NC));
     if (c->keys) {
       uint64_t h = arg_hash(1469598103934665603ull, f);
-      const int cfg[8] = {o.dir, Q, S_run, depth, (nan_check && !c->eff) ? 1 : 0, c->shared,
-                          NC, c->pipe_pf};
+      const int cfg[9] = {o.dir, Q, S_run, depth, (nan_check && !c->eff) ? 1 : 0, c->shared,
+                          NC, c->pipe_pf, pf};
       c->keys->push_back(arg_hash(h, cfg));
     }
     if (c->dry) {
@@ -667,7 +717,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     } else if (Q > 1) {
       launch_sweep_group(o.dir, Q, f, nb_run, c->stream);
     } else {
-      launch_sweep_fast(o.dir, S_run, depth, nan_check && !c->eff, c->shared != 0, f,
+      launch_sweep_fast(o.dir, S_run, depth, pf, nan_check && !c->eff, c->shared != 0, f,
                         c->nblocks, c->stream);
     }
   } else {
@@ -845,7 +895,7 @@ const char* const kOptionNames[] = {"prefetch_depth", "shared", "shared_max_bloc
                                     "precontract", "depth4_max_blocks", "pair_max_blocks",
                                     "quad_max_blocks", "red_rows", "red_stage", "group_q",
                                     "fused_update", "graph", "pipe", "pipe_pf", "pipe_min_blocks", "rec_sweep",
-                                    "pipe_max_blocks", nullptr};
+                                    "pipe_max_blocks", "prefetch_steps", nullptr};
 int set_option(frei_ctx* c, const std::string& k, int v) {
   if (k == "prefetch_depth") c->prefetch_depth = v;
   else if (k == "shared") c->shared_mode = v < 0 ? -1 : (v ? 1 : 0);
@@ -864,6 +914,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "rec_sweep") c->rec_sweep = v < 0 ? -1 : (v ? 1 : 0);
   else if (k == "pipe_max_blocks") c->pipe_max_blocks = v;
   else if (k == "pipe_pf") c->pipe_pf = v == 1 ? 1 : 2;
+  else if (k == "prefetch_steps") c->prefetch_steps = v >= 16 ? 16 : v >= 8 ? 8 : 0;
   else return fail("unknown option '" + k + "'");
   c->meta_dirty = true;
   return 0;
@@ -1879,6 +1930,13 @@ int frei_set_option(frei_ctx* c, const char* name, int value) {
 int frei_setup_timing(frei_ctx* c, double* ms) {
   if (!c || !ms) return fail("null argument");
   for (int k = 0; k < 5; ++k) ms[k] = c->setup_ms[k];
+  return 0;
+}
+
+int frei_contract_timing(frei_ctx* c, double* ms, double* bytes) {
+  if (!c || !ms || !bytes) return fail("null argument");
+  *ms = c->contract_ms;
+  *bytes = c->contract_bytes;
   return 0;
 }
 

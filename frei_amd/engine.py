@@ -317,6 +317,13 @@ class Engine:
         return dict(zip(("brackets_host", "uploads", "eff_alloc", "eff_zero", "contract"),
                         ms.tolist()))
 
+    def contract_timing(self):
+        """The last species-contraction kernel (K3, or K7 for a batched context): dict(ms = its
+        HIP-event duration, bytes = its algorithmic HBM bytes) (frei_contract_timing)."""
+        ms, nb = ctypes.c_double(0), ctypes.c_double(0)
+        N.check(N.lib().frei_contract_timing(self._ctx, ctypes.byref(ms), ctypes.byref(nb)))
+        return dict(ms=ms.value, bytes=nb.value)
+
     def kappa(self, T, p_bar):
         k = np.empty(self.n_lam)
         sig = np.empty(self.n_lam)

@@ -237,6 +237,12 @@ int frei_graph_info(frei_ctx* ctx, int* captures, int* replays);
  * host, [1] metadata uploads, [2] contracted-table allocation, [3] its zero fill, [4] the K3
  * contraction kernel. */
 int frei_setup_timing(frei_ctx* ctx, double* ms5);
+/* The last species-contraction launch (K3 for one atmosphere, K7 on fp64 MFMA for a batched
+ * context; part of the metadata build): its duration by HIP events on the context stream, ms,
+ * and its algorithmic HBM bytes (the S tables' used pressure rows read once, one contracted
+ * table per atmosphere written).  0 / 0 before any contraction.  (No reference counterpart:
+ * the reference sums species inside every kappa call, opacity.py:250-268.) */
+int frei_contract_timing(frei_ctx* ctx, double* ms, double* bytes);
 
 /* Timing of the sweep kernel (HIP events on the context stream around every sweep
  * launch while enabled): total milliseconds and number of timed launches. */

@@ -808,3 +808,46 @@ def test_high_albedo_lanes_match_oracle(fa, monkeypatch, precontract):
         assert_flux_parity(down, od, cond["down"], delta, what + " F_down")
         assert_grid_parity(r["spectrum"], osp, up, ou, down, od, what, floor,
                            T=r["final_T"], ref_T=oT)
+
+
+@pytest.mark.parametrize("depth,pf", [(2, 8), (2, 16), (4, 8), (4, 16)])
+@pytest.mark.parametrize("n_layers", [5, 34, 60])
+def test_deep_prefetch_sweep_is_bitwise_the_one_lane_form(fa, monkeypatch, depth, pf, n_layers):
+    """FREI_PREFETCH_STEPS: the contracted one-lane sweep with its loads issued 8 or 16 steps
+    ahead (a register ring) runs the same arithmetic in the same order, so one sweep each way
+    and a T-P run are bit-identical to the default distance (5 layers: fewer steps than the
+    ring; 34 / 60: partial last rounds)."""
+    rng = np.random.default_rng(19)
+    lam, _, _ = O.wavelength_grid(0.5, 10, 3000)
+    p = O.pressure_grid(n_layers, -6, np.log10(200))
+    T0 = O.temperature_grid(p, 1600.0, 0.1, 0.1)
+    Tn = np.linspace(0.8 * T0.min(), 1.2 * T0.max(), 9)
+    names = ["1H2-16O", "12C-16O"]
+    tabs = {n: fa.SeparableTable(10 ** rng.uniform(-4, 2, lam.size), (p / 1.0) ** 0.1,
+                                 (Tn / 1000.0) ** 0.5, p, Tn) for n in names}
+    mmr = O.mock_mmr(names, M_BAR)[:, None] * np.ones(n_layers)
+    monkeypatch.setenv("FREI_GROUP_Q", "1")
+    monkeypatch.setenv("FREI_PIPE", "0")
+    monkeypatch.setenv("FREI_PREFETCH_DEPTH", str(depth))
+    out = {}
+    for steps in (0, pf):
+        monkeypatch.setenv("FREI_PREFETCH_STEPS", str(steps))
+        eng = fa.Engine(lam, p, tabs, mmr=mmr)
+        try:
+            assert eng.path()["contracted"]
+            r = {}
+            for d in (0, 1):
+                eng.set_temperatures(T0)
+                eng.set_fluxes(np.full((n_layers, lam.size), 1e9),
+                               np.full((n_layers, lam.size), 2e8))
+                r[d] = eng.sweep(d, alpha=1.0) + eng.get_fluxes()
+            r["run"] = eng.run(T0, n_timesteps=4, n_zero_crossings=10 ** 6, convergence_dT=-1.0)
+            out[steps] = r
+        finally:
+            eng.close()
+    a, b = out[pf], out[0]
+    for d in (0, 1):
+        for x, y in zip(a[d], b[d]):
+            assert np.array_equal(x, y), (depth, pf, d)
+    for k in ("final_T", "spectrum", "dtaus"):
+        assert np.array_equal(a["run"][k], b["run"][k]), k
