@@ -120,6 +120,9 @@ class BatchEngine:
     def setup_timing(self):
         return Engine.setup_timing(self)
 
+    def set_option(self, name, value):
+        return Engine.set_option(self, name, value)
+
     def contract_timing(self):
         return Engine.contract_timing(self)
 

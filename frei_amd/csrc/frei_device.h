@@ -403,6 +403,9 @@ void launch_contribution(const double* dtaus, int nL, int64_t n, const double* n
 void launch_contract_batch(const double* const* tabs, int S, const double* mmr,
                            const int32_t* prow, int n_layers, int n_T, int64_t pitch,
                            int n_atm, int64_t tab_stride, double* eff, hipStream_t st);
+void launch_contract_batch_valu(const double* const* tabs, int S, const double* mmr,
+                           const int32_t* prow, int n_layers, int n_T, int64_t pitch,
+                           int n_atm, int64_t tab_stride, double* eff, hipStream_t st);
 void launch_contract(const double* const* tabs, int S, const double* mmr, const int32_t* prow,
                      int n_layers, int n_T, int64_t pitch, double* eff, hipStream_t st);
 

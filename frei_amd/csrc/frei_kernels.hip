@@ -368,6 +368,16 @@ __device__ __forceinline__ double stream_load(const double* p) {
 #endif
 }
 
+// Scheduling fence of the sweep's load ring (FREI_RING_FENCE=0: none, A/B).
+#ifndef FREI_RING_FENCE
+#define FREI_RING_FENCE 1
+#endif
+__device__ __forceinline__ void ring_fence() {
+#if FREI_RING_FENCE
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
 // Carry-independent part of one step (everything in twostream.py:135-176 except the
 // terms that multiply the carried flux).  Split out so two layers' coefficients form one
 // straight-line block the scheduler interleaves (2x instruction-level parallelism per
@@ -583,8 +593,11 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   // last one), so they need no step-table read
   auto layer_of = [&](int k) { return step_layer(DIR, k, ns + 1); };
   auto top_of = [&](int k) { return DIR == kEmit && k == ns - 1; };
-  auto load = [&](int k, double (&v)[2 * S], double& stale) {
-    k = k < ns ? k : ns - 1;  // unconditional (clamped) loads keep vmcnt waits counted
+  // Loads of a step: the 2S table rows (with shared brackets the row offset comes from the
+  // step table) and the stale opposite-stream flux.  Unconditional, at clamped indices, so the
+  // vmcnt bookkeeping stays static.
+  auto load_rows = [&](int k, double (&v)[2 * S]) {
+    k = k < ns ? k : ns - 1;
 #ifdef FREI_CACHEONLY   // diagnostic build: same instructions, loads from a cache-resident 32 KB
     {
       const int64_t jj = j & 2047;
@@ -593,23 +606,17 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
         v[2 * s] = stream_load(a.tab[s] + jj + (k & 1) * 2048);
         v[2 * s + 1] = stream_load(a.tab[s] + jj + 4096);
       }
-      stale = Fu[jj + (k & 1) * 2048];
       return;
     }
 #endif
     if constexpr (SH) {
       const int64_t off = uni(sp[k].off);
-      const int layer = layer_of(k);
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const double* r = a.tab[s] + off + j;
         v[2 * s] = stream_load(r);
         v[2 * s + 1] = stream_load(r + a.pitch);
       }
-      const double* src = (DIR == kEmit)
-                              ? (top_of(k) ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
-                              : Fu + (int64_t)layer * nl;
-      stale = src[j];
       return;
     }
 #pragma unroll
@@ -618,31 +625,21 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       v[2 * s] = stream_load(r);
       v[2 * s + 1] = stream_load(r + a.pitch);
     }
+  };
+  auto load_stale = [&](int k, double& stale) {
+    k = k < ns ? k : ns - 1;
+#ifdef FREI_CACHEONLY
+    stale = Fu[(j & 2047) + (k & 1) * 2048];
+    return;
+#endif
     const int i = layer_of(k);
     const double* src = (DIR == kEmit) ? (top_of(k) ? a.ftoa : Fd + (int64_t)(i + 1) * nl)
                                        : Fu + (int64_t)i * nl;
     stale = src[j];
   };
-  // Phase A of step k from buffer v (then refilled with step k + PD): opacity, dtau,
-  // single-scattering albedo and the Planck terms, everything before E.
-  // Bprev: emit -> B(T1) of this step, absorb -> B(T2) of this step (reuse, Q: B2 = next B1).
-  auto coef = [&](int k, double (&v)[2 * S], double& stale, double Bprev, StepCoef& c,
-                  PreCoef& pc) {
+  // Species-summed opacity of step k from its row slot (opacity.py:250-269).
+  auto opacity = [&](int k, const double (&v)[2 * S]) {
     const int kk = k < ns ? k : ns - 1;  // the last pair of a PD = 2 loop may be a dummy
-    double iT1, iT2, dm;   // inverse temperatures of the step's layers
-    if constexpr (SH) {
-      c.layer = layer_of(kk);
-      c.top = top_of(kk);
-      iT1 = UNIV(sp[kk].iT1);
-      iT2 = UNIV(sp[kk].iT2);
-      dm = UNIV(sp[kk].dm);
-    } else {
-      c.layer = layer_of(kk);
-      c.top = top_of(kk);
-      iT1 = st[kk].iT1;
-      iT2 = st[kk].iT2;
-      dm = st[kk].dm;
-    }
     double tot = 0.0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -661,8 +658,27 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       if (NANCHK && S > 1) ops = isnan(ops) ? 0.0 : ops;
       tot = (s == 0) ? ops : tot + ops;
     }
-    c.F_st = stale;
-    load(k + PF, v, stale);
+    return tot;
+  };
+  // Phase A of step k from its opacity: dtau, single-scattering albedo and the Planck terms,
+  // everything before E.
+  // Bprev: emit -> B(T1) of this step, absorb -> B(T2) of this step (reuse, Q: B2 = next B1).
+  auto coef = [&](int k, double tot, double Bprev, StepCoef& c, PreCoef& pc) {
+    const int kk = k < ns ? k : ns - 1;
+    double iT1, iT2, dm;   // inverse temperatures of the step's layers
+    if constexpr (SH) {
+      c.layer = layer_of(kk);
+      c.top = top_of(kk);
+      iT1 = UNIV(sp[kk].iT1);
+      iT2 = UNIV(sp[kk].iT2);
+      dm = UNIV(sp[kk].dm);
+    } else {
+      c.layer = layer_of(kk);
+      c.top = top_of(kk);
+      iT1 = st[kk].iT1;
+      iT2 = st[kk].iT2;
+      dm = st[kk].dm;
+    }
     const double kap = tot + sig;
     const double dtau = dm * kap;
     const double w0 = fm::div(sig, sig + kap);
@@ -707,9 +723,9 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
 
   // Carry-dependent finish of step k: fluxes, stores, bolometric partials.
   double carry;
-  auto finish = [&](int k, const StepCoef& c) {
+  auto finish = [&](int k, const StepCoef& c, double F_st) {
     double F1u, F2d;
-    if (DIR == kEmit) { F1u = carry; F2d = c.F_st; } else { F2d = carry; F1u = c.F_st; }
+    if (DIR == kEmit) { F1u = carry; F2d = F_st; } else { F2d = carry; F1u = F_st; }
     const double F2u = c.ic * ((c.psi * F1u - c.xi * F2d) + c.Xu);
     const double F1d = c.ic * ((c.psi * F2d - c.xi * F1u) + c.Xd);
     if (k >= ns) return;
@@ -760,9 +776,18 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   }
   // PD steps in flight: their loads are issued PD steps ahead, their coefficients form one
   // block (PD-way instruction-level parallelism), then the short carried recurrence.
+  // Ring of PF steps' loads: slot (k mod PF) is refilled with step k + PF as soon as step k
+  // has consumed it — the rows after the opacity sums, the stale flux after the flux update —
+  // and a scheduling fence keeps every refill behind the last read of the slot's old value, so
+  // the old and new values never live at once: each slot stays one register pair across the
+  // loop's back edge, with no copy there (a copy of a register whose load is in flight would
+  // make the compiler drain every outstanding load at the latch, vmcnt(0)).
   double vb[PF][2 * S], sb[PF];
 #pragma unroll
-  for (int b = 0; b < PF; ++b) load(b, vb[b], sb[b]);
+  for (int b = 0; b < PF; ++b) {
+    load_rows(b, vb[b]);
+    load_stale(b, sb[b]);
+  }
   for (int k0 = 0; k0 < ns; k0 += PF) {
 #pragma unroll
   for (int g = 0; g < PF / PD; ++g) {
@@ -770,16 +795,25 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     if (PF > PD && k >= ns) break;   // wave-uniform: no dummy coefficient blocks at the end
     StepCoef c[PD];
     PreCoef pc[PD];
+    double tot[PD];
+#pragma unroll
+    for (int b = 0; b < PD; ++b) tot[b] = opacity(k + b, vb[g * PD + b]);
+    ring_fence();
+#pragma unroll
+    for (int b = 0; b < PD; ++b) load_rows(k + b + PF, vb[g * PD + b]);
     double Bp = Bc;
 #pragma unroll
     for (int b = 0; b < PD; ++b) {
-      coef(k + b, vb[g * PD + b], sb[g * PD + b], Bp, c[b], pc[b]);
+      coef(k + b, tot[b], Bp, c[b], pc[b]);
       Bp = c[b].Bnext;
     }
     Bc = Bp;
     coefB(pc, c);
 #pragma unroll
-    for (int b = 0; b < PD; ++b) finish(k + b, c[b]);
+    for (int b = 0; b < PD; ++b) finish(k + b, c[b], sb[g * PD + b]);
+    ring_fence();
+#pragma unroll
+    for (int b = 0; b < PD; ++b) load_stale(k + b + PF, sb[g * PD + b]);
     if constexpr (PD == 2) {
       if (a.red_rows == 2) {   // the pair's 8 (step, quantity) sums over the wave's 64 lanes
         __builtin_amdgcn_wave_barrier();
@@ -2099,14 +2133,23 @@ struct ContractArgs {
   int64_t pitch;
 };
 
+// S is a template parameter so every species' load is issued at once (kernel-argument table
+// pointers at constant indices); two adjacent columns per lane (16-B loads and stores).  The
+// sum keeps the species order: eff = mmr_0 tab_0, then eff + mmr_s tab_s.
+typedef double dbl2k3 __attribute__((ext_vector_type(2)));
+template <int S>
 __global__ __launch_bounds__(256) void contract_kernel(ContractArgs a) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= a.pitch) return;
+  const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  if (j >= a.pitch) return;   // the pitch is a multiple of 64
   const int l = blockIdx.y, t = blockIdx.z;
   const int64_t idx = ((int64_t)a.prow[l] * a.n_T + t) * a.pitch + j;
-  double acc = a.mmr[l] * a.tab[0][idx];
-  for (int s = 1; s < a.S; ++s) acc = acc + a.mmr[(int64_t)s * a.n_layers + l] * a.tab[s][idx];
-  a.eff[idx] = acc;
+  dbl2k3 v[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) v[s] = *reinterpret_cast<const dbl2k3*>(a.tab[s] + idx);
+  dbl2k3 acc = a.mmr[l] * v[0];
+#pragma unroll
+  for (int s = 1; s < S; ++s) acc = acc + a.mmr[(int64_t)s * a.n_layers + l] * v[s];
+  *reinterpret_cast<dbl2k3*>(a.eff + idx) = acc;
 }
 
 void launch_contract(const double* const* tabs, int S, const double* mmr, const int32_t* prow,
@@ -2120,8 +2163,13 @@ void launch_contract(const double* const* tabs, int S, const double* mmr, const 
   a.n_layers = n_layers;
   a.n_T = n_T;
   a.pitch = pitch;
-  dim3 grid((unsigned)((pitch + 255) / 256), (unsigned)n_layers, (unsigned)n_T);
-  hipLaunchKernelGGL(contract_kernel, grid, dim3(256), 0, st, a);
+  dim3 grid((unsigned)((pitch / 2 + 255) / 256), (unsigned)n_layers, (unsigned)n_T);
+  switch (S) {
+#define K3(n) case n: hipLaunchKernelGGL(contract_kernel<n>, grid, dim3(256), 0, st, a); break;
+    K3(1) K3(2) K3(3) K3(4) K3(5) K3(6) K3(7)
+    default: hipLaunchKernelGGL(contract_kernel<8>, grid, dim3(256), 0, st, a);
+#undef K3
+  }
 }
 
 // ---------------------------------------------------------------- post-processing
@@ -2293,6 +2341,7 @@ __device__ __forceinline__ void k7_store(dbl2* p, dbl2 v) {
 #endif
 }
 
+template <int S>
 __global__ __launch_bounds__(256) void contract_batch_kernel(ContractBatchArgs a) {
   __shared__ double tile[4][kK7Rows * kK7Row];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2301,15 +2350,28 @@ __global__ __launch_bounds__(256) void contract_batch_kernel(ContractBatchArgs a
   const int64_t col0 = ((int64_t)blockIdx.x * 4 + wv) * kK7Cols;
   const int64_t rowbase = (int64_t)a.prow[l] * ncol;
   const int ci = lane & 15, kq = lane >> 4;   // column in the tile, species in the K step
-  constexpr int kSteps = kMaxFastS / 4;
+  // S is a template parameter: the species' table pointers are kernel-argument constants and
+  // every load is unconditional (clamped column, zero weight for padded species), so all of
+  // them are in flight at once — a runtime-indexed pointer array made each load a dependent
+  // round trip (kernarg load, then the data, vmcnt(0) after each)
+  constexpr int kSteps = (S + 3) / 4;
+  const double* tp[kSteps];
+#pragma unroll
+  for (int ks = 0; ks < kSteps; ++ks) {
+    const double* p = a.tab[0];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * ks + q < S && kq == q) p = a.tab[4 * ks + q];
+    tp[ks] = p;
+  }
   double b[kK7Tiles][kSteps];
 #pragma unroll
   for (int t = 0; t < kK7Tiles; ++t)
 #pragma unroll
     for (int ks = 0; ks < kSteps; ++ks) {
-      const int s = 4 * ks + kq;
-      const int64_t c = col0 + 16 * t + ci;
-      b[t][ks] = (s < a.S && c < ncol) ? a.tab[s][rowbase + c] : 0.0;
+      const int64_t c = min(col0 + 16 * t + ci, ncol - 1);
+      const double v = tp[ks][rowbase + c];
+      b[t][ks] = (4 * ks + kq < S) ? v : 0.0;
     }
   double* my = tile[wv];
   for (int m0 = 0; m0 < a.n_atm; m0 += 16) {
@@ -2318,18 +2380,15 @@ __global__ __launch_bounds__(256) void contract_batch_kernel(ContractBatchArgs a
 #pragma unroll
     for (int ks = 0; ks < kSteps; ++ks) {
       const int s = 4 * ks + kq;
-      av[ks] = (am < a.n_atm && s < a.S) ? a.mmr[((int64_t)am * a.S + s) * a.n_layers + l]
-                                         : 0.0;
+      av[ks] = (am < a.n_atm && s < S) ? a.mmr[((int64_t)am * S + s) * a.n_layers + l] : 0.0;
     }
     dbl4 acc[kK7Tiles];
 #pragma unroll
     for (int t = 0; t < kK7Tiles; ++t) {
       acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int ks = 0; ks < kSteps; ++ks) {
-        if (4 * ks >= a.S) break;
+      for (int ks = 0; ks < kSteps; ++ks)
         acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], b[t][ks], acc[t], 0, 0, 0);
-      }
     }
     // D: this lane holds rows kq + 4 r (atmospheres) of column 16 t + ci
 #pragma unroll
@@ -2359,6 +2418,68 @@ __global__ __launch_bounds__(256) void contract_batch_kernel(ContractBatchArgs a
   }
 }
 
+// K7, VALU form: one lane per pair of adjacent columns (16-B loads and stores, 1 KiB per
+// wave-instruction), the S table values held in registers and every atmosphere's sum formed in
+// K3's species order — eff = mmr_0 tab_0, then eff + mmr_s tab_s — so each atmosphere's
+// contracted table is bit for bit the one K3 builds for that atmosphere alone; the mixing
+// ratios are wave-uniform (scalar loads).  The contraction is 0.125 flop per byte: HBM, not the
+// arithmetic, bounds it, and this form reaches the store probe's rate (tools/store_probe.hip).
+constexpr int kK7Chunk = 64;   // atmospheres whose mixing ratios are staged in LDS at a time
+
+template <int S>
+__global__ __launch_bounds__(256) void contract_batch_valu_kernel(ContractBatchArgs a) {
+  __shared__ double smm[kK7Chunk * S];   // [atmosphere][species] of this layer
+  const int l = blockIdx.y;
+  const int64_t ncol = (int64_t)a.n_T * a.pitch;   // even (pitch is a multiple of 64)
+  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+  const bool live = c < ncol;
+  const int64_t at = (int64_t)a.prow[l] * ncol + (live ? c : 0);
+  dbl2 v[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) v[s] = *reinterpret_cast<const dbl2*>(a.tab[s] + at);
+  for (int m0 = 0; m0 < a.n_atm; m0 += kK7Chunk) {
+    const int nm = min(kK7Chunk, a.n_atm - m0);
+    if (m0 > 0) __syncthreads();   // the previous chunk's ratios are no longer read
+    for (int q = threadIdx.x; q < nm * S; q += 256) {
+      const int m = q / S, s = q - m * S;
+      smm[q] = a.mmr[((int64_t)(m0 + m) * S + s) * a.n_layers + l];
+    }
+    __syncthreads();
+    if (live)
+      for (int m = 0; m < nm; ++m) {
+        const double* mm = smm + m * S;
+        dbl2 acc = mm[0] * v[0];
+#pragma unroll
+        for (int s = 1; s < S; ++s) acc = acc + mm[s] * v[s];
+        *reinterpret_cast<dbl2*>(a.eff + (int64_t)(m0 + m) * a.tab_stride + at) = acc;
+      }
+  }
+}
+
+void launch_contract_batch_valu(const double* const* tabs, int S, const double* mmr,
+                                const int32_t* prow, int n_layers, int n_T, int64_t pitch,
+                                int n_atm, int64_t tab_stride, double* eff, hipStream_t st) {
+  ContractBatchArgs a{};
+  for (int s = 0; s < S && s < kMaxFastS; ++s) a.tab[s] = tabs[s];
+  a.mmr = mmr;
+  a.prow = prow;
+  a.eff = eff;
+  a.S = S;
+  a.n_layers = n_layers;
+  a.n_T = n_T;
+  a.n_atm = n_atm;
+  a.pitch = pitch;
+  a.tab_stride = tab_stride;
+  const int64_t ncol = (int64_t)n_T * pitch;
+  dim3 grid((unsigned)((ncol / 2 + 255) / 256), (unsigned)n_layers);
+  switch (S) {
+#define K7V(n) case n: hipLaunchKernelGGL(contract_batch_valu_kernel<n>, grid, dim3(256), 0, st, a); break;
+    K7V(1) K7V(2) K7V(3) K7V(4) K7V(5) K7V(6) K7V(7)
+    default: hipLaunchKernelGGL(contract_batch_valu_kernel<8>, grid, dim3(256), 0, st, a);
+#undef K7V
+  }
+}
+
 void launch_contract_batch(const double* const* tabs, int S, const double* mmr,
                            const int32_t* prow, int n_layers, int n_T, int64_t pitch,
                            int n_atm, int64_t tab_stride, double* eff, hipStream_t st) {
@@ -2375,7 +2496,12 @@ void launch_contract_batch(const double* const* tabs, int S, const double* mmr,
   a.tab_stride = tab_stride;
   const int64_t ncol = (int64_t)n_T * pitch;
   dim3 grid((unsigned)((ncol + 4 * kK7Cols - 1) / (4 * kK7Cols)), (unsigned)n_layers);
-  hipLaunchKernelGGL(contract_batch_kernel, grid, dim3(256), 0, st, a);
+  switch (S) {
+#define K7M(n) case n: hipLaunchKernelGGL(contract_batch_kernel<n>, grid, dim3(256), 0, st, a); break;
+    K7M(1) K7M(2) K7M(3) K7M(4) K7M(5) K7M(6) K7M(7)
+    default: hipLaunchKernelGGL(contract_batch_kernel<8>, grid, dim3(256), 0, st, a);
+#undef K7M
+  }
 }
 
 __global__ void fill_kernel(double* x, int64_t n, double v) {

@@ -176,6 +176,7 @@ struct frei_ctx {
   void* comm = nullptr;
   int nranks = 1, rank = 0;
   int prefetch_depth = 0;               // 0 = automatic (FREI_PREFETCH_DEPTH overrides)
+  int k7_mfma = 1;                      // FREI_K7_MFMA: batched contraction on MFMA (1) or VALU (0)
   int prefetch_steps = 0;               // FREI_PREFETCH_STEPS: contracted one-lane sweep's load
                                         // distance in steps (0 = automatic, 8 / 16 = deeper)
   // Shared-bracket kernel (step table staged in LDS): used when every species shares its
@@ -356,9 +357,12 @@ int build_contracted(frei_ctx* c, bool shared_fast, Lap&& lap) {
   if (hipEventCreate(&k0) != hipSuccess || hipEventCreate(&k1) != hipSuccess)
     return fail("hipEventCreate failed");
   HIP_TRY(hipEventRecord(k0, c->stream));
-  if (batch)  // K7: [n_atm x S] . [S x n_T*pitch] per layer on fp64 MFMA
+  if (batch && c->k7_mfma)  // K7: [n_atm x S] . [S x n_T*pitch] per layer on fp64 MFMA
     launch_contract_batch(tabs, S, c->d_mmr, c->d_prow, nL, q0.n_T, q0.stride, c->n_atm,
                           (int64_t)per, c->d_eff, c->stream);
+  else if (batch)           // K7 on the VALU, K3's species order
+    launch_contract_batch_valu(tabs, S, c->d_mmr, c->d_prow, nL, q0.n_T, q0.stride,
+                               c->n_atm, (int64_t)per, c->d_eff, c->stream);
   else
     launch_contract(tabs, S, c->d_mmr, c->d_prow, nL, q0.n_T, q0.stride, c->d_eff, c->stream);
   HIP_TRY(hipGetLastError());
@@ -895,7 +899,7 @@ const char* const kOptionNames[] = {"prefetch_depth", "shared", "shared_max_bloc
                                     "precontract", "depth4_max_blocks", "pair_max_blocks",
                                     "quad_max_blocks", "red_rows", "red_stage", "group_q",
                                     "fused_update", "graph", "pipe", "pipe_pf", "pipe_min_blocks", "rec_sweep",
-                                    "pipe_max_blocks", "prefetch_steps", nullptr};
+                                    "pipe_max_blocks", "prefetch_steps", "k7_mfma", nullptr};
 int set_option(frei_ctx* c, const std::string& k, int v) {
   if (k == "prefetch_depth") c->prefetch_depth = v;
   else if (k == "shared") c->shared_mode = v < 0 ? -1 : (v ? 1 : 0);
@@ -914,6 +918,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "rec_sweep") c->rec_sweep = v < 0 ? -1 : (v ? 1 : 0);
   else if (k == "pipe_max_blocks") c->pipe_max_blocks = v;
   else if (k == "pipe_pf") c->pipe_pf = v == 1 ? 1 : 2;
+  else if (k == "k7_mfma") c->k7_mfma = v != 0;
   else if (k == "prefetch_steps") c->prefetch_steps = v >= 16 ? 16 : v >= 8 ? 8 : 0;
   else return fail("unknown option '" + k + "'");
   c->meta_dirty = true;

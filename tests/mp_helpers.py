@@ -9,6 +9,7 @@ bit-reproducible.  One process per GPU — the production layout
 a device, so only these tests need it.
 """
 import ctypes
+import os
 import socket
 
 _KEEP = []
@@ -16,7 +17,7 @@ _KEEP = []
 
 def offset_device_allocations(rank, device=0, step_mib=1536):
     """Allocate (and keep) rank * step_mib MiB on ``device`` before the rank's engine."""
-    if rank <= 0:
+    if rank <= 0 or os.environ.get("FREI_TEST_NO_VA_OFFSET") == "1":
         return
     hip = ctypes.CDLL("libamdhip64.so")
     assert hip.hipSetDevice(device) == 0

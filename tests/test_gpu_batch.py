@@ -44,7 +44,9 @@ def _setup(fa, n_atm, n_lam, n_layers, names, seed):
     return lam, p, tabs_o, tabs_f, g, mmr, T0
 
 
-def test_batched_atmospheres_match_oracle_per_atmosphere(fa):
+@pytest.mark.parametrize("k7_mfma", ["1", "0"])
+def test_batched_atmospheres_match_oracle_per_atmosphere(fa, monkeypatch, k7_mfma):
+    monkeypatch.setenv("FREI_K7_MFMA", k7_mfma)   # K7 on MFMA / on the VALU
     names = ["1H2-16O", "12C-16O", "Na"]
     lam, p, tabs_o, tabs_f, g, mmr, T0 = _setup(fa, 5, 2048, 30, names, 17)
     Ft = O.F_TOA(lam)
@@ -74,9 +76,12 @@ def test_batched_atmospheres_match_oracle_per_atmosphere(fa):
                            floor, T=out["final_T"][m], ref_T=oT)
 
 
-def test_batched_mfma_contraction_tiles_and_padding(fa):
+@pytest.mark.parametrize("k7_mfma", ["1", "0"])
+def test_batched_mfma_contraction_tiles_and_padding(fa, monkeypatch, k7_mfma):
     """17 atmospheres (two 16-row MFMA tiles, one padded) x 5 species (a padded K step):
-    fixed-work iterations agree with one single-atmosphere engine per atmosphere."""
+    fixed-work iterations agree with one single-atmosphere engine per atmosphere (both K7
+    forms; the VALU form sums the species in K3's order)."""
+    monkeypatch.setenv("FREI_K7_MFMA", k7_mfma)
     names = ["1H2-16O", "12C-16O", "12C-16O2", "Na", "K"]
     lam, p, tabs_o, tabs_f, g, mmr, T0 = _setup(fa, 17, 700, 16, names, 23)
     eng = fa.BatchEngine(lam, p, tabs_f, g=g, mmr=mmr)
@@ -91,6 +96,7 @@ def test_batched_mfma_contraction_tiles_and_padding(fa):
         N.check(N.lib().frei_get_temperatures(eng._ctx, N.dptr(Tb)))
     finally:
         eng.close()
+    monkeypatch.delenv("FREI_K7_MFMA")
     for m in (0, 7, 16):
         single = fa.Engine(lam, p, tabs_f, g=g[m], mmr=mmr[m])
         try:
