@@ -375,13 +375,6 @@ def main():
 
     n_dev = max(1, N.device_count())
     if d.world > n_dev:   # rehearsal on fewer GPUs than ranks: ranks share the GPUs there are
-        if d.local >= n_dev:
-            # ranks sharing a device need distinct device address layouts
-            import ctypes
-            hip = ctypes.CDLL("libamdhip64.so")
-            hip.hipSetDevice(d.local % n_dev)
-            _pad = ctypes.c_void_p()
-            hip.hipMalloc(ctypes.byref(_pad), ctypes.c_size_t((d.local // n_dev) * 1536 << 20))
         d.local = d.local % n_dev
         # the producer/consumer sweep takes a whole CU per block (VGPRs and LDS); next to other
         # ranks' update kernels spinning on the same GPU for their peers' sums its blocks can

@@ -1,29 +1,14 @@
 """Helpers for multi-process tests that put several ranks on ONE GPU (test infrastructure).
 
-Ranks sharing a device must not have identical device virtual-address layouts: with two
-processes that allocate the same buffer sequence (same virtual addresses) running kernels
-concurrently on one MI355X, values read through the per-CU caches were intermittently wrong
-(different on every run; 1-process runs are bit-reproducible).  Shifting each rank's
-allocations by a dummy allocation of its own size made every such run correct and
-bit-reproducible.  One process per GPU — the production layout — never shares
-a device, so only these tests need it.
+Round 2 offset each rank's device allocations here, after multi-rank runs on one GPU had
+intermittently produced wrong temperatures.  Round 3 attributed that: the engine-free probe
+(tools/va_probe.hip, profiles/r03/va_probe.txt) shows that two processes never get identical
+device virtual addresses (ASLR) and read no foreign values in 6.9e10 reads, and the multi-rank
+tests pass without the offset (3 of 3 runs, profiles/r03/multirank_no_offset.txt).  The effect
+came from the table-padding memset on the null stream racing the context's stream, fixed in
+round 2 after the offset was introduced.  The offset is gone.
 """
-import ctypes
-import os
 import socket
-
-_KEEP = []
-
-
-def offset_device_allocations(rank, device=0, step_mib=1536):
-    """Allocate (and keep) rank * step_mib MiB on ``device`` before the rank's engine."""
-    if rank <= 0 or os.environ.get("FREI_TEST_NO_VA_OFFSET") == "1":
-        return
-    hip = ctypes.CDLL("libamdhip64.so")
-    assert hip.hipSetDevice(device) == 0
-    p = ctypes.c_void_p()
-    assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(rank * step_mib << 20)) == 0
-    _KEEP.append(p)
 
 
 def free_port():

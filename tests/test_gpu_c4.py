@@ -53,8 +53,6 @@ def _rank(rank, world, port, transport, q, chem=False):
         from frei_amd.distributed import host_comm, p2p_comm, partition
         from frei_amd.engine import Engine
         from frei_amd.rendezvous import Rendezvous
-        from tests.mp_helpers import offset_device_allocations
-        offset_device_allocations(rank)       # ranks share device 0 (tests/mp_helpers.py)
         rdzv = Rendezvous(world, rank, addr=("127.0.0.1", port), timeout=180)
         w, tabs = _tables()
         lo, hi = partition(w["lam"].size, world, rank)

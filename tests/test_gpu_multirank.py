@@ -31,8 +31,6 @@ def _worker(rank, world, port, transport, q):
         from frei_amd.distributed import host_comm, p2p_comm, partition
         from frei_amd.engine import Engine
         from frei_amd.rendezvous import Rendezvous
-        from tests.mp_helpers import offset_device_allocations
-        offset_device_allocations(rank)       # ranks share device 0 (tests/mp_helpers.py)
         rdzv = Rendezvous(world, rank, addr=("127.0.0.1", port), timeout=120)
         grid, op = _problem()
         lo, hi = partition(grid.lam.size, world, rank)
@@ -90,8 +88,6 @@ def _silent_worker(rank, world, port, q, hold_s):
         from frei_amd.distributed import p2p_comm, partition
         from frei_amd.engine import Engine
         from frei_amd.rendezvous import Rendezvous
-        from tests.mp_helpers import offset_device_allocations
-        offset_device_allocations(rank)
         rdzv = Rendezvous(world, rank, addr=("127.0.0.1", port), timeout=120)
         grid, op = _problem()
         lo, hi = partition(grid.lam.size, world, rank)
