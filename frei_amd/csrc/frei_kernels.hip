@@ -417,11 +417,13 @@ struct StepCoef {
 // Terms after E (twostream.py:143-176), same expression order as two_stream().  pi_w =
 // pi (1 - w0) / (E - w0) comes from the caller; 1 / chi is formed within an ulp (it scales
 // the whole update, nothing cancels after it); the transmission's exp argument is <= 0.
+// NF: the step's inputs cannot be NaN (contracted-table sweeps), so exp's clamp is a max.
+template <bool NF = false>
 __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, double B2,
                                           double sq, double r, double q, double pi_w,
                                           StepCoef& c) {
   (void)w0;
-  const double Tr = fm::exp_neg((-2.0 * sq) * dtau);
+  const double Tr = NF ? fm::exp_neg_nf((-2.0 * sq) * dtau) : fm::exp_neg((-2.0 * sq) * dtau);
   const double zp = 0.5 * (1.0 + r);
   const double zm = 0.5 * (1.0 - r);
   const double Tr2 = Tr * Tr;
@@ -439,6 +441,7 @@ __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, dou
 }
 
 // General step (twostream.py:139-176): E of Deitrick 2020 Eqn 19 where w0 > 0.1, else 1.
+template <bool NF = false>
 __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, double B2,
                                           StepCoef& c) {
   const double E = (w0 > 0.1) ? ((1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0)) : 1.0;
@@ -450,7 +453,8 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
 #else
   const double pi_w = fm::div(kPi * (1.0 - w0), Emw);
 #endif
-  coef_tail(w0, dtau, B1, B2, fm::sqrt(E * Emw), fm::sqrt(fm::div(Emw, E)), q, pi_w, c);
+  coef_tail<NF>(w0, dtau, B1, B2, fm::sqrt_pos(E * Emw), fm::sqrt_pos(fm::div(Emw, E)), q,
+                pi_w, c);
 }
 
 // Step whose w0 <= 0.1 (E = 1): E * Emw, Emw / E and Bprime / (2 E) are exact without the
@@ -458,15 +462,16 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
 // square root with bit-identical results.  pi (1 - w0) / (1 - w0) is pi within an ulp (the
 // reference's own rounding of it), so the constant replaces a third division.  Taken when
 // the whole wave qualifies.
+template <bool NF = false>
 __device__ __forceinline__ void coef_e1(double w0, double dtau, double B1, double B2,
                                         StepCoef& c) {
   const double Emw = 1.0 - w0;
-  const double sq = fm::sqrt(Emw);
+  const double sq = fm::sqrt_pos(Emw);
 #if FREI_PI_E1
-  coef_tail(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5, kPi, c);
+  coef_tail<NF>(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5, kPi, c);
 #else
-  coef_tail(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5,
-            fm::div(kPi * (1.0 - w0), Emw), c);
+  coef_tail<NF>(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5,
+                fm::div(kPi * (1.0 - w0), Emw), c);
 #endif
 }
 
@@ -546,6 +551,10 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
   static_assert(PD == 1 || PD == 2 || PD == 4, "prefetch depth 1, 2 or 4");
   static_assert(PF % PD == 0, "prefetch distance: a multiple of the coefficient block");
   static_assert(!MM1 || S == 1, "mmr = 1 only for the contracted single table");
+  // no NaN reaches the coefficients: the contracted table is built from NaN-free tables, and
+  // with S > 1 the tables were scanned (NaN-free, or NANCHK's nansum zeroes NaN terms); only a
+  // single per-species table keeps the reference's NaN propagation (Q8)
+  constexpr bool kNaNFree = MM1 || S > 1;
   {  // atmosphere of a batched launch (identity for one atmosphere)
     const int m = blockIdx.y;
     Fu += m * a.bs.flux;
@@ -713,10 +722,12 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     for (int b = 0; b < PD; ++b) e1 = e1 && !(pc[b].w0 > 0.1);
     if (__all(e1)) {
 #pragma unroll
-      for (int b = 0; b < PD; ++b) coef_e1(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2, c[b]);
+      for (int b = 0; b < PD; ++b)
+        coef_e1<kNaNFree>(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2, c[b]);
     } else {
 #pragma unroll
-      for (int b = 0; b < PD; ++b) coef_from(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2, c[b]);
+      for (int b = 0; b < PD; ++b)
+        coef_from<kNaNFree>(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2, c[b]);
     }
 #endif
   };
@@ -1076,11 +1087,11 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     phaseA(g + 1, pb, A1);   // a dummy group past the end is computed, not stored
     StepCoef c0, c1;
     if (__all(!(A0.w0 > 0.1) && !(A1.w0 > 0.1))) {
-      coef_e1(A0.w0, A0.dtau, A0.B1, A0.B2, c0);
-      coef_e1(A1.w0, A1.dtau, A1.B1, A1.B2, c1);
+      coef_e1<true>(A0.w0, A0.dtau, A0.B1, A0.B2, c0);   // contracted table: NaN-free
+      coef_e1<true>(A1.w0, A1.dtau, A1.B1, A1.B2, c1);
     } else {
-      coef_from(A0.w0, A0.dtau, A0.B1, A0.B2, c0);
-      coef_from(A1.w0, A1.dtau, A1.B1, A1.B2, c1);
+      coef_from<true>(A0.w0, A0.dtau, A0.B1, A0.B2, c0);
+      coef_from<true>(A1.w0, A1.dtau, A1.B1, A1.B2, c1);
     }
     finish(A0, c0);
     if (g + 1 < ng) finish(A1, c1);
@@ -1277,10 +1288,12 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
       for (int i = 0; i < M; ++i) e1 = e1 && !(pc[i].w0 > 0.1);
       if (__all(e1)) {
 #pragma unroll
-        for (int i = 0; i < M; ++i) coef_e1(pc[i].w0, pc[i].dtau, pc[i].B1, pc[i].B2, c[i]);
+        for (int i = 0; i < M; ++i)   // contracted table: NaN-free
+          coef_e1<true>(pc[i].w0, pc[i].dtau, pc[i].B1, pc[i].B2, c[i]);
       } else {
 #pragma unroll
-        for (int i = 0; i < M; ++i) coef_from(pc[i].w0, pc[i].dtau, pc[i].B1, pc[i].B2, c[i]);
+        for (int i = 0; i < M; ++i)
+          coef_from<true>(pc[i].w0, pc[i].dtau, pc[i].B1, pc[i].B2, c[i]);
       }
 #pragma unroll
       for (int i = 0; i < M; ++i) {

@@ -209,6 +209,28 @@ __device__ __forceinline__ double exp_neg(double x) {
   return __builtin_ldexp(p, (int)n);
 }
 
+// exp_neg for an argument that cannot be NaN (the contracted-table sweeps: K3 is only built
+// for NaN-free tables): the clamp is one v_max_f64 instead of a compare and two selects (maxNum
+// would turn a NaN into -1100; here there is none).  Bit-identical to exp_neg otherwise.
+__device__ __forceinline__ double exp_neg_nf(double x) {
+  x = __builtin_fmax(x, -1100.0);
+  const double n = __builtin_rint(x * c64(0x3ff71547652b82feull));
+  double r = __builtin_fma(c64(0xbfe62e42fefa39efull), n, x);
+  r = __builtin_fma(c64(0xbc7abc9e3b39803full), n, r);
+  double p = __builtin_fma(c64(0x3e5ade156a5dcb37ull), r, c64(0x3e928af3fca7ab0cull));
+  p = hfma(r, p, 0x3ec71dee623fde64ull);
+  p = hfma(r, p, 0x3efa01997c89e6b0ull);
+  p = hfma(r, p, 0x3f2a01a014761f6eull);
+  p = hfma(r, p, 0x3f56c16c1852b7b0ull);
+  p = hfma(r, p, 0x3f81111111122322ull);
+  p = hfma(r, p, 0x3fa55555555502a1ull);
+  p = hfma(r, p, 0x3fc5555555555511ull);
+  p = hfma(r, p, 0x3fe000000000000bull);
+  p = __builtin_fma(r, p, 1.0);
+  p = __builtin_fma(r, p, 1.0);
+  return __builtin_ldexp(p, (int)n);
+}
+
 // 1 / b within one ulp: the reciprocal part of the division core below (rcp and two
 // Newton-Raphson steps) without the quotient's final residual correction.  Used where the
 // result only scales a sum (1 / chi of the flux update), so an ulp is not amplified.
@@ -266,6 +288,26 @@ __device__ __forceinline__ double sqrt(double x) {
   g = __builtin_fma(d, h, g);
 #endif
   return __builtin_amdgcn_class(x, 0x260) ? x : g;   // +-0, +inf
+}
+
+// sqrt(x) for the sweep's square roots — E (E - w0), (E - w0) / E and 1 - w0 with
+// w0 = sigma / (2 sigma + sum of table terms) <= 1/2 and E in [1, 1.21], i.e. x in (1/2, 1.21]
+// for non-negative opacities: sqrt's sequence without the +-0 / +inf pass-through (three
+// instructions), which only differs at exactly those inputs; NaN propagates as before.
+__device__ __forceinline__ double sqrt_pos(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y;
+  double h = y * 0.5;
+  const double e = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, e, g);
+  h = __builtin_fma(h, e, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+#if FREI_FM_SQRT != 2
+  d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+#endif
+  return g;
 }
 
 }  // namespace fm
