@@ -937,10 +937,14 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   const int64_t sstep = (DIR == kEmit ? (int64_t)Q : -(int64_t)Q) * nl;
   const double* pst = (DIR == kEmit) ? Fd + (int64_t)(q + 2) * nl + j
                                      : Fu + (int64_t)(nL - 2 - q) * nl + j;
-  int kl = q;                        // this lane's step of the next load
-  auto load = [&](int g, Pre& P) {
-    (void)g;
-    const FastStepS& st = sp[clampk(kl)];
+  // Two loads per group buffer, each issued once the buffer's previous value is consumed (the
+  // one-lane sweep's load ring, ring_fence): the table rows and step parameters right after
+  // the opacity, the stale flux after the group's flux update — so no buffer value is live
+  // across its refill and the loop's back edge needs no register copies (a copy of an
+  // in-flight load drains every outstanding load there).
+  int kr = q, kst = q;               // this lane's step of the next row / stale load
+  auto load_rows = [&](Pre& P) {
+    const FastStepS& st = sp[clampk(kr)];
     const double* r = tabj + st.off;
     P.wl = st.wlo;
     P.wh = st.whi;
@@ -948,12 +952,15 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     P.iT = DIR == kEmit ? st.iT2 : st.iT1;
     P.vlo = stream_load(r);
     P.vhi = stream_load(r + a.pitch);
+    kr += Q;
+  };
+  auto load_stale = [&](Pre& P) {
     // emit's top step reads F_TOA; past the last step (dummy groups) any valid row serves
-    const double* src = (DIR == kEmit) ? (kl >= ns - 1 ? ftoaj : pst)
-                                       : (kl >= ns ? Fu + j : pst);
+    const double* src = (DIR == kEmit) ? (kst >= ns - 1 ? ftoaj : pst)
+                                       : (kst >= ns ? Fu + j : pst);
     P.stale = *src;
     pst += sstep;
-    kl += Q;
+    kst += Q;
   };
   double carry, carryB;
   {
@@ -967,19 +974,19 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     }
   }
   struct GroupA {
-    double w0, dtau, B1, B2, F_st;
+    double w0, dtau, B1, B2;
     int k;
   };
   // Phase A of this lane's step in group g (opacity, dtau, albedo, Planck chain of the
-  // group); refills the group's buffer with group g + 2.
+  // group); refills the group's row buffer with group g + 2.
   auto phaseA = [&](int g, Pre& P, GroupA& A) {
     const int k = Q * g + q;
     A.k = k;
-    A.F_st = P.stale;
     // contracted table: mmr = 1, and (0 + a) + b == a + b for its non-negative terms
     const double kap = (P.vlo * P.wl + P.vhi * P.wh) + sig;
     const double dm = P.dm, iTnew = P.iT;
-    load(g + 2, P);
+    ring_fence();
+    load_rows(P);
     A.dtau = dm * kap;
     A.w0 = fm::div(sig, sig + kap);
     // each lane forms its step's new Planck value; the group gathers them and resolves
@@ -1009,8 +1016,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   double* pt = (dtaus ? dtaus : Fu) + (int64_t)(q + 1) * nl + j;
   // Carried recurrence through the group (steps in order), stores of this lane's step and
   // the reduction of the group's bolometric terms.
-  auto finish = [&](const GroupA& A, const StepCoef& c) {
-    const double F_st = A.F_st;
+  auto finish = [&](const GroupA& A, const StepCoef& c, const double F_st) {
     // the two fluxes of a step from its carried input (same expressions as the one-lane form)
     auto flux_up = [&](double in) {   // F_2_up
       const double F1u = (DIR == kEmit) ? in : F_st, F2d = (DIR == kEmit) ? F_st : in;
@@ -1079,8 +1085,10 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   };
   const int ng = (ns + Q - 1) / Q;
   Pre pa, pb;                      // two groups in flight (4: measured no faster)
-  load(0, pa);
-  load(1, pb);
+  load_rows(pa);
+  load_stale(pa);
+  load_rows(pb);
+  load_stale(pb);
   for (int g = 0; g < ng; g += 2) {
     GroupA A0, A1;
     phaseA(g, pa, A0);
@@ -1093,8 +1101,11 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
       coef_from<true>(A0.w0, A0.dtau, A0.B1, A0.B2, c0);
       coef_from<true>(A1.w0, A1.dtau, A1.B1, A1.B2, c1);
     }
-    finish(A0, c0);
-    if (g + 1 < ng) finish(A1, c1);
+    finish(A0, c0, pa.stale);
+    if (g + 1 < ng) finish(A1, c1, pb.stale);
+    ring_fence();
+    load_stale(pa);
+    load_stale(pb);
     if (a.red_rows == 2) {
       // the 8Q (group, quantity, step residue) sums of the two groups over the wave's 64/Q
       // wavelengths: 8/Q lanes per output, each adds 8 staged values (residue qq, lanes
@@ -1282,6 +1293,7 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
           Bp = pc[i].B1;
         }
       }
+      ring_fence();   // every read of b above precedes its refill
       load(ph + PF, b);
       bool e1 = true;
 #pragma unroll
@@ -1496,8 +1508,13 @@ __device__ __forceinline__ void p2p_wait(const P2PWait& w, int r, int64_t idx, l
 // The acquire that pairs with p2p_push_values' system-scope release: issued after the flag
 // waits and before any p2p_value, so the value loads cannot be performed (by the compiler or
 // the memory system) ahead of the flag loads that observed this sweep's sequence number.
+#ifndef FREI_P2P_ACQ   // A/B only (0: no fence; the value loads then rely on issue order)
+#define FREI_P2P_ACQ 1
+#endif
 __device__ __forceinline__ void p2p_acquire() {
+#if FREI_P2P_ACQ
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
 }
 
 // Rank r's value idx of this sweep (after p2p_wait + p2p_acquire); the mailbox is uncached

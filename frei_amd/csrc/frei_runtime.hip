@@ -190,8 +190,11 @@ struct frei_ctx {
   int pair_max_blocks = 420;            // FREI_PAIR_MAX_BLOCKS (<= 107k lambda per GPU)
   int quad_max_blocks = 208;            // FREI_QUAD_MAX_BLOCKS (<= 53k lambda per GPU)
   int group_q = 0;                      // FREI_GROUP_Q forces 1, 2 or 4 lanes per wavelength
-  int pipe_nc = -1;                     // FREI_PIPE: producer/consumer sweep, 1/2/4 consumers per
-                                        // block, 0 off, -1 by slice size (pipe_*_blocks)
+  int pipe_nc = 0;                      // FREI_PIPE: producer/consumer sweep, 1/2/4 consumers per
+                                        // block, 0 off (default since round 3: two lanes per
+                                        // wavelength with in-sweep records give the shorter
+                                        // T-P iteration at 62.5k, profiles/r03/slice_forms.txt),
+                                        // -1 by slice size (pipe_*_blocks)
   int pipe_min_blocks = 208;            // FREI_PIPE_MIN_BLOCKS / _MAX_BLOCKS: 256-wavelength
   int pipe_max_blocks = -1;             // blocks per GPU where the auto choice takes NC = 4
                                         // (-1: the CU count, one 16-wave block per CU)
