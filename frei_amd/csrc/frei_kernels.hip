@@ -22,6 +22,36 @@
 
 namespace frei {
 
+// ---------------------------------------------------------------- diagnostic trace
+// FREI_TRACE builds only (tools/trace_probe.py): thread 0 of every block of the sweeps and
+// the fused update appends (kernel kind, block, 4 wall-clock marks at 100 MHz) to a device
+// ring — entry, end of the prologue, end of the main loop, exit — so one T-P half-iteration's
+// launch latency, prologue, steps and drain can be read off without a profiler.
+#ifdef FREI_TRACE
+struct TraceRec {
+  long long kind, block, t[4];
+};
+constexpr unsigned kTraceCap = 1u << 17;
+__device__ TraceRec g_trace[kTraceCap];
+__device__ unsigned int g_trace_n;
+#define TRACE_DECL long long tr_[4] = {wall_clock64(), 0, 0, 0}
+#define TRACE_MARK(i) (tr_[i] = wall_clock64())
+#define TRACE_PUT(kind)                                                      \
+  do {                                                                       \
+    tr_[3] = wall_clock64();                                                 \
+    if (threadIdx.x == 0) {                                                  \
+      const unsigned i_ = atomicAdd(&g_trace_n, 1u);                         \
+      if (i_ < kTraceCap)                                                    \
+        g_trace[i_] = TraceRec{(kind), (long long)blockIdx.x,                \
+                               {tr_[0], tr_[1], tr_[2], tr_[3]}};            \
+    }                                                                        \
+  } while (0)
+#else
+#define TRACE_DECL
+#define TRACE_MARK(i)
+#define TRACE_PUT(kind)
+#endif
+
 // ---------------------------------------------------------------- device math
 // twostream.py:64-67: 2hc^2/lam^5 / expm1(hc / (lam k T)).  The exponent is formed as
 // (hc / (lam k)) * (1 / T) — a per-wavelength constant (host) times a per-layer one (the step
@@ -568,6 +598,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     a.conv += m;
   }
   if (!a.force && *a.conv) return;
+  TRACE_DECL;
   extern __shared__ double red[];  // [wave][step][4], then (shared brackets) the step table
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -596,6 +627,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     }
     sp = reinterpret_cast<const FastStepS*>(lss);
   }
+  TRACE_MARK(1);
   // Load the 2S table rows and the stale opposite-stream flux of step k into one buffer
   // (and, with shared brackets, the step's uniform parameters).
   // a step's layer and top flag follow from its index (step_layer; emit's top step is the
@@ -845,6 +877,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     }
   }
   }
+  TRACE_MARK(2);
   __syncthreads();
   for (int idx = tid; idx < ns * 4; idx += kBlock) {
     double s = red[idx];
@@ -852,6 +885,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
       s += red[(int64_t)w * ns * 4 + idx];
     part[(int64_t)idx * gridDim.x + blockIdx.x] = s;
   }
+  TRACE_PUT(1);
 }
 
 // ---------------------------------------------------------------- K1, grouped-lane form
@@ -894,6 +928,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     a.conv += m;
   }
   if (!a.force && *a.conv) return;
+  TRACE_DECL;
   extern __shared__ double red[];  // [wave][step][4], then the step table
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -920,6 +955,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     }
   }
   const FastStepS* sp = reinterpret_cast<const FastStepS*>(lss);
+  TRACE_MARK(1);
   auto clampk = [&](int k) { return k < ns ? k : ns - 1; };
   const int nL = ns + 1;
   // A step's layer and top flag follow from its index (step_layer; emit's top step is the
@@ -1127,6 +1163,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
       __builtin_amdgcn_wave_barrier();
     }
   }
+  TRACE_MARK(2);
   __syncthreads();
   for (int idx = tid; idx < ns * 4; idx += kBlock) {
     double s = red[idx];
@@ -1134,6 +1171,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
       s += red[(int64_t)w * ns * 4 + idx];
     part[(int64_t)idx * gridDim.x + blockIdx.x] = s;
   }
+  TRACE_PUT(10 + Q);
 }
 
 // Q lanes per wavelength: kBlock / Q wavelengths per block.
@@ -1209,6 +1247,7 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
     a.conv += m;
   }
   if (!a.force && *a.conv) return;
+  TRACE_DECL;
   extern __shared__ double lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1238,6 +1277,7 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
     for (int idx = tid; idx < ns * kStepDoubles; idx += 256 * NC) l[idx] = g[idx];
     __syncthreads();
   }
+  TRACE_MARK(1);
   auto rslot = [&](int ph, int s, int v) {
     return ring + ((((ph & 1) * G + s) * kPipeNV + v) << 6) + lane;
   };
@@ -1406,12 +1446,14 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
       __syncthreads();
     }
   }
+  TRACE_MARK(2);
   __syncthreads();
   for (int idx = tid; idx < ns * 4; idx += 256 * NC) {
     double s = red[idx];
     for (int w = 1; w < NC; ++w) s += red[(int64_t)w * ns * 4 + idx];
     part[(int64_t)idx * gridDim.x + blockIdx.x] = s;
   }
+  TRACE_PUT(20 + NC);
 }
 
 template <int DIR, int NC, int M, int PF>
@@ -1926,6 +1968,7 @@ __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a)
 #ifdef FREI_UPD_EMPTY  // diagnostic ablation build: launch floor
   return;
 #endif
+  TRACE_DECL;
   const int l = blockIdx.x;
   const int nL = a.su.n_layers;
   const int dir = a.dir;
@@ -2011,6 +2054,7 @@ __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a)
     if (tid == 1 && l + 1 < nL) sTn[l + 1] = T1;      // layer l + 1 before its update
   }
   __syncthreads();
+  TRACE_MARK(1);
   if (tid < 8) {
     double t = wsum[0][tid];
     for (int w = 1; w < kRedWaves; ++w) t += wsum[w][tid];
@@ -2097,6 +2141,7 @@ __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a)
       }
     }
   }
+  TRACE_MARK(2);
   __syncthreads();   // sTn of layers l, l + 1
 #ifndef FREI_UPD_NOSETUP  // diagnostic ablation build
   if (kn >= 0 && tid >= 64) {
@@ -2108,6 +2153,7 @@ __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a)
                   kn + 1, tid - 64, blockDim.x - 64, nL, 0);
   }
 #endif
+  TRACE_PUT(30);
 }
 
 // ---------------------------------------------------------------- standalone kernels
@@ -2699,3 +2745,19 @@ void launch_fill(double* x, int64_t n, double v, hipStream_t st) {
 }
 
 }  // namespace frei
+
+#ifdef FREI_TRACE
+// Diagnostic builds only: copy out (and reset) the trace ring.  rec: n_max x 6 int64
+// (kind, block, 4 wall-clock marks); *n: records written since the last reset.
+extern "C" int frei_trace_fetch(long long* rec, int n_max, int* n) {
+  unsigned cnt = 0;
+  if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(frei::g_trace_n), sizeof(cnt)) != hipSuccess) return -1;
+  const unsigned m = cnt < (unsigned)n_max ? cnt : (unsigned)n_max;
+  if (m && hipMemcpyFromSymbol(rec, HIP_SYMBOL(frei::g_trace), m * sizeof(frei::TraceRec)) !=
+               hipSuccess)
+    return -1;
+  *n = (int)cnt;
+  const unsigned zero = 0;
+  return hipMemcpyToSymbol(HIP_SYMBOL(frei::g_trace_n), &zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
