@@ -276,7 +276,21 @@ struct FastArgs {
   // previous update kernel wrote; rec holds the setup inputs (T of this sweep).
   int rec_on;
   SetupArgs rec;
+  int min_lds;             // minimum dynamic LDS bytes per block (caps blocks per CU; launch only)
+  // Chained launch (sweep_chain_kernel: its leading workgroups run the previous sweep's fused
+  // update): the sweep blocks poll rec.T — kPoisonT until that update publishes each value —
+  // and *ch_epoch for its convergence decision, instead of waiting for a kernel boundary.
+  const unsigned long long* ch_epoch;   // [n_layers] the update's granules; nullptr: not chained
+  unsigned long long ch_val;            // epoch value this launch waits for
+  int ch_can_conv;                      // the update is the convergence test (tracked absorb)
+  long long ch_timeout;                 // wall_clock64 ticks before a wait gives up
+  int* ch_err;                          // set to 1 when a wait gave up
+  // the deferred update's output temperatures: block 0 fills them with kPoisonT (nullptr: none)
+  double* poison;
 };
+// "not yet published" pattern of a chained temperature: a signalling NaN, which no arithmetic
+// produces (results are quiet NaNs), so a diverged run's NaN temperature is still a value
+constexpr unsigned long long kPoisonT = 0xFFF4F4F4F4F4F4F4ull;
 
 struct SweepArgs {
   int64_t n_lam;
@@ -346,6 +360,11 @@ struct UpdateArgs {
   P2PPush push;
   double* T_out;
   unsigned* done;
+  // chained into the next sweep's launch (sweep_chain_kernel): T_out published by sc1 stores,
+  // and per layer l the granule epoch[l] = (epoch_val << 2) | (converged before << 1) |
+  // (layer converged) (nullptr: a launch of its own)
+  unsigned long long* epoch;
+  unsigned long long epoch_val;
 };
 
 // LDS bytes of the update kernel (K4/K5): T, dT, p, T before/after absorb, ln p ratios,
@@ -362,9 +381,14 @@ __host__ __device__ inline size_t update_lds_bytes(int nL, int ntn, int S, bool 
 void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st);
 void launch_sweep_fast(int dir, int S, int depth, int pf, bool nan_check, bool shared,
                        const FastArgs& a, int nblocks, hipStream_t st);
-// Grouped-lane sweep (Q = 2 or 4 lanes per wavelength, 256/Q wavelengths per block):
+// Grouped-lane sweep (Q = 2 or 4 lanes per wavelength, NW = 4 or 8 waves per block, 64 NW / Q
+// wavelengths per block):
 // contracted single table, step table in LDS; for slices with about one wave per SIMD.
-void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStream_t st);
+void launch_sweep_group(int dir, int Q, int NW, const FastArgs& a, int nblocks, hipStream_t st);
+// The grouped-lane sweep chained to the previous sweep's fused update u (one launch: u's
+// workgroups first, then the sweep blocks, which poll the new temperatures; single atmosphere).
+void launch_sweep_chain(int dir, int Q, int NW, const FastArgs& a, const UpdateArgs& u,
+                        int nblocks, hipStream_t st);
 // producer/consumer sweep: NC consumer waves (64 NC wavelengths) per block, table rows PF
 // phases ahead
 void launch_sweep_pipe(int dir, int NC, int PF, const FastArgs& a, int nblocks, hipStream_t st);

@@ -17,6 +17,8 @@
 // Numerics: fp64 throughout, compiled with -ffp-contract=off and the reference's
 // expression order, so results differ from NumPy only by the last-ulp differences of
 // exp/expm1/sqrt (ocml vs libm).  See DESIGN.md "Parity".
+#include <unordered_map>
+
 #include "frei_device.h"
 #include "frei_math.h"
 
@@ -517,15 +519,15 @@ struct PreCoef {
 //      of both steps in a per-wave LDS tile; then every lane sums 8 consecutive lanes of one
 //      of the 8 (step, quantity) outputs and three DPP levels finish the 64-lane sums —
 //      about a third of the VALU work of a per-step butterfly, no block barrier.
-__host__ __device__ inline int red_rows_per_block(int red_rows) {
-  return (kBlock / 64) * (red_rows == 1 ? 4 : 1);
+__host__ __device__ inline int red_rows_per_block(int red_rows, int nw = kBlock / 64) {
+  return nw * (red_rows == 1 ? 4 : 1);
 }
 // mode 2 tile: [wave][2 steps][4 quantities][64 lanes + 8 pad]; the pad staggers the rows
 // over the LDS banks so the strided reads of the reduction are conflict-free
 constexpr int kStageRow = 72;
-constexpr int kStageDoubles = (kBlock / 64) * 2 * 4 * kStageRow;
-__host__ __device__ inline int64_t red_lds_doubles(int red_rows, int ns) {
-  return (int64_t)red_rows_per_block(red_rows) * ns * 4 + (red_rows == 2 ? kStageDoubles : 0);
+__host__ __device__ inline int64_t red_lds_doubles(int red_rows, int ns, int nw = kBlock / 64) {
+  return (int64_t)red_rows_per_block(red_rows, nw) * ns * 4 +
+         (red_rows == 2 ? (int64_t)nw * 2 * 4 * kStageRow : 0);
 }
 
 // The sweep's step records formed in its own prologue (FastArgs.rec_on: contracted table,
@@ -540,8 +542,32 @@ __device__ inline void atm_view(SetupArgs& u, int m);
 __host__ __device__ inline int64_t rec_scratch_doubles(const FastArgs& a) {
   return a.rec_on ? 2 * (int64_t)a.rec.n_layers + a.rec.n_tnodes : 0;
 }
-__device__ __forceinline__ void stage_records(const FastArgs& a, int dir, FastStepS* dst,
-                                           double* scratch) {
+// Chained launch: a temperature the leading update workgroups publish by one write-through
+// (sc1) store; polled by sc1 loads (global, never flat: they bypass this CU's L1) until it is
+// no longer kPoisonT — the value is its own ready flag (an 8-byte granule, MI355X_MICROARCH.md
+// "Valid forms" R2).  A bounded wait: after ch_timeout it flags ch_err and returns what it read.
+using gu64 = __attribute__((address_space(1))) unsigned long long;
+__device__ __forceinline__ unsigned long long chain_poll(const FastArgs& a, const void* p,
+                                                         unsigned long long until_not,
+                                                         unsigned long long want, bool eq) {
+  const gu64* g = (const gu64*)p;
+  unsigned long long v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long t0 = wall_clock64();
+  while (eq ? (v >> 2) != want : v == until_not) {
+    __builtin_amdgcn_s_sleep(1);
+    v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wall_clock64() - t0 > a.ch_timeout) {
+      __hip_atomic_store(a.ch_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+  return v;
+}
+
+// Returns 1 (every thread, after a barrier) when a chained launch's update found the run
+// converged: the caller's sweep block then returns, as an unchained sweep would at entry.
+__device__ __forceinline__ int stage_records(const FastArgs& a, int dir, FastStepS* dst,
+                                          double* scratch) {
   SetupArgs u = a.rec;
   if (a.n_atm > 1) atm_view(u, blockIdx.y);
   const int nL = u.n_layers, ns = nL - 1, ntn = u.n_tnodes;
@@ -549,15 +575,31 @@ __device__ __forceinline__ void stage_records(const FastArgs& a, int dir, FastSt
   double* sT = scratch;
   double* sP = sT + nL;
   double* sN = sP + nL;
+  int skip = 0, allc = 1;   // chained: run already converged / every layer converged
   for (int q = tid; q < nL; q += nthr) {
-    sT[q] = u.T[q];
+    if (a.ch_epoch) {
+      sT[q] = __builtin_bit_cast(double, chain_poll(a, u.T + q, kPoisonT, 0, false));
+      const unsigned long long g = chain_poll(a, a.ch_epoch + q, 0, a.ch_val, true);
+      skip |= (int)((g >> 1) & 1);
+      allc &= (int)(g & 1);
+    } else {
+      sT[q] = u.T[q];
+    }
     sP[q] = u.p[q];
   }
   for (int q = tid; q < ntn; q += nthr) sN[q] = u.tnodes[q];
   // this thread's first record's metadata, loaded with T / p (one global round trip in all)
   const SpecMeta sm = u.spec[0];
   const PMeta pm0 = u.pmeta[step_layer(dir, tid < ns ? tid : 0, nL)];
-  __syncthreads();
+  if (a.ch_epoch) {
+    // the update's convergence decision, formed from its per-layer granules: the sweep does
+    // not run once the run has converged (as an unchained sweep returns at entry)
+    skip = __syncthreads_or(skip);
+    allc = __syncthreads_and(allc);
+    if ((skip || (a.ch_can_conv && allc)) && !a.force) return 1;
+  } else {
+    __syncthreads();
+  }
   for (int k = tid; k < ns; k += nthr) {
     FastStepS f;
     step_s_core(u, sT, sP, sN, sm, k == tid ? pm0 : u.pmeta[step_layer(dir, k, nL)], dir, k,
@@ -567,6 +609,7 @@ __device__ __forceinline__ void stage_records(const FastArgs& a, int dir, FastSt
     dst[k] = f;
   }
   __syncthreads();
+  return 0;
 }
 
 // PD steps form one coefficient block; PF (a multiple of PD) is the prefetch distance: the
@@ -619,7 +662,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     double* lss = red + red_lds_doubles(a.red_rows, ns);
     constexpr int kW = sizeof(FastStepS) / sizeof(double);
     if (a.rec_on) {   // form the records here from the current T (the update wrote none)
-      stage_records(a, DIR, reinterpret_cast<FastStepS*>(lss), lss + ns * kW);
+      (void)stage_records(a, DIR, reinterpret_cast<FastStepS*>(lss), lss + ns * kW);
     } else {
       const double* g = reinterpret_cast<const double*>(ss);
       for (int idx = tid; idx < ns * kW; idx += kBlock) lss[idx] = g[idx];
@@ -911,11 +954,17 @@ __device__ __forceinline__ double from_lane(double x) {
 }
 
 
-template <int DIR, int Q>
-__global__ __launch_bounds__(kBlock) void sweep_group_kernel(
-    FastArgs a, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
-    double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
+// Block bx of nbx sweep blocks (a chained launch's sweep blocks follow its update workgroups);
+// red: the dynamic LDS.  CH: chained — the temperatures and the convergence decision come from
+// the leading update workgroups (stage_records polls them).
+template <int DIR, int Q, int NW, bool CH>
+__device__ __forceinline__ void sweep_group_body(
+    FastArgs& a, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
+    double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus,
+    double* red, const int bx, const int nbx) {
   static_assert(Q == 2 || Q == 4, "2 or 4 lanes per wavelength");
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves per block");
+  constexpr int kB = 64 * NW;   // threads per block
   {  // atmosphere of a batched launch (identity for one atmosphere)
     const int m = blockIdx.y;
     Fu += m * a.bs.flux;
@@ -927,15 +976,20 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     a.ftoa += m * a.bs.ftoa;
     a.conv += m;
   }
-  if (!a.force && *a.conv) return;
+  if (!CH && !a.force && *a.conv) return;
   TRACE_DECL;
-  extern __shared__ double red[];  // [wave][step][4], then the step table
+  // red: [wave][step][4], then the step table
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
   const int q = lane & (Q - 1);    // step residue this lane computes
   const int64_t nl = a.n_lam;
-  const int64_t j0 = (int64_t)blockIdx.x * (kBlock / Q) + wv * (64 / Q) + lane / Q;
+  // the deferred update's output temperatures start as "not published" (its own launch reads
+  // them only after this one has ended)
+  if (a.poison && bx == 0)
+    for (int i = tid; i <= a.n_steps; i += kB)
+      reinterpret_cast<unsigned long long*>(a.poison)[i] = kPoisonT;
+  const int64_t j0 = (int64_t)bx * (kB / Q) + wv * (64 / Q) + lane / Q;
   const bool act = j0 < nl;
   const int64_t j = act ? j0 : nl - 1;
   const double c1 = a.c1[j], hcl = a.hcl[j], sig = a.sig[j];
@@ -943,14 +997,14 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   const int ns = a.n_steps;
   const fm::Expm1Reg ek = fm::expm1_regs();
   const double* __restrict__ tab = a.tab[0];
-  double* lss = red + red_lds_doubles(a.red_rows, ns);
+  double* lss = red + red_lds_doubles(a.red_rows, ns, NW);
   {
     constexpr int kW = sizeof(FastStepS) / sizeof(double);
     if (a.rec_on) {   // form the records here from the current T (the update wrote none)
-      stage_records(a, DIR, reinterpret_cast<FastStepS*>(lss), lss + ns * kW);
+      if (stage_records(a, DIR, reinterpret_cast<FastStepS*>(lss), lss + ns * kW)) return;
     } else {
       const double* g = reinterpret_cast<const double*>(ss);
-      for (int idx = tid; idx < ns * kW; idx += kBlock) lss[idx] = g[idx];
+      for (int idx = tid; idx < ns * kW; idx += kB) lss[idx] = g[idx];
       __syncthreads();
     }
   }
@@ -1098,7 +1152,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
     pd += rstep;
     pt += (int64_t)Q * nl;
     if (a.red_rows == 2) {   // staged: reduced per pair of groups (below, main loop)
-      double* t = red + (int64_t)(kBlock / 64) * ns * 4 +
+      double* t = red + (int64_t)NW * ns * 4 +
                   ((wv * 2 + ((k / Q) & 1)) * 4) * kStageRow + lane;
       t[0] = wt * F2u;
       t[kStageRow] = wt * F2d;
@@ -1126,6 +1180,13 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   load_rows(pb);
   load_stale(pb);
   for (int g = 0; g < ng; g += 2) {
+    // 8 waves: two per SIMD from ONE block, held level by a barrier every two group pairs —
+    // left alone, the older wave takes the issue slots first and the younger one finishes
+    // its last groups alone at single-wave speed (two 4-wave blocks per CU: the second-placed
+    // blocks ended ~10 us after the first at 62.5k, profiles/r03/trace_blocks_62500.txt)
+    if constexpr (NW == 8) {
+      if ((g & 3) == 0) __syncthreads();
+    }
     GroupA A0, A1;
     phaseA(g, pa, A0);
     phaseA(g + 1, pb, A1);   // a dummy group past the end is computed, not stored
@@ -1150,7 +1211,7 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
       constexpr int L = 8 / Q;                       // lanes per output
       const int o = lane / L, r = lane % L;
       const int p = o / (4 * Q), qi = (o / Q) & 3, qq = o % Q;
-      const double* t = red + (int64_t)(kBlock / 64) * ns * 4 +
+      const double* t = red + (int64_t)NW * ns * 4 +
                         ((wv * 2 + p) * 4 + qi) * kStageRow + qq + Q * r;
       double y = t[0];
 #pragma unroll
@@ -1165,35 +1226,67 @@ __global__ __launch_bounds__(kBlock) void sweep_group_kernel(
   }
   TRACE_MARK(2);
   __syncthreads();
-  for (int idx = tid; idx < ns * 4; idx += kBlock) {
+  for (int idx = tid; idx < ns * 4; idx += kB) {
     double s = red[idx];
-    for (int w = 1; w < red_rows_per_block(a.red_rows); ++w)
+    for (int w = 1; w < red_rows_per_block(a.red_rows, NW); ++w)
       s += red[(int64_t)w * ns * 4 + idx];
-    part[(int64_t)idx * gridDim.x + blockIdx.x] = s;
+    part[(int64_t)idx * nbx + bx] = s;
   }
-  TRACE_PUT(10 + Q);
+  TRACE_PUT(CH ? 40 + Q : 10 + Q);
 }
 
-// Q lanes per wavelength: kBlock / Q wavelengths per block.
-void launch_sweep_group(int dir, int Q, const FastArgs& a, int nblocks, hipStream_t st) {
-  const size_t shm = (size_t)red_lds_doubles(a.red_rows, a.n_steps) * sizeof(double) +
+template <int DIR, int Q, int NW>
+__global__ __launch_bounds__(64 * NW) void sweep_group_kernel(
+    FastArgs a, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
+    double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
+  extern __shared__ double red[];
+  sweep_group_body<DIR, Q, NW, false>(a, ss, Fu, Fd, part, dtaus, red, blockIdx.x, gridDim.x);
+}
+
+
+// Dynamic LDS of a one-lane / grouped-lane sweep launch: at least a.min_lds bytes
+// (FREI_SWEEP_LDS_KB), which caps the blocks resident per CU at 160 KiB / min_lds, so the
+// dispatcher cannot stack three or four blocks on one CU while others hold one (small slices:
+// the launch ends with its most loaded CU).  Above 64 KiB the kernel opts in first.
+static size_t sweep_shm(const void* kernel, const FastArgs& a, size_t shm) {
+  const size_t s = shm > (size_t)a.min_lds ? shm : (size_t)a.min_lds;
+  if (s > 65536) {
+    static std::unordered_map<const void*, size_t> optin;
+    size_t& have = optin[kernel];
+    if (s > have) {
+      (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s);
+      have = s;
+    }
+  }
+  return s;
+}
+
+// Q lanes per wavelength, NW waves: 64 NW / Q wavelengths per block.
+void launch_sweep_group(int dir, int Q, int NW, const FastArgs& a, int nblocks,
+                        hipStream_t st) {
+  const size_t shm = (size_t)red_lds_doubles(a.red_rows, a.n_steps, NW) * sizeof(double) +
                      (size_t)a.n_steps * sizeof(FastStepS) +
                      (size_t)rec_scratch_doubles(a) * sizeof(double);
   const dim3 grid(nblocks, a.n_atm > 1 ? a.n_atm : 1);
-  if (Q == 4) {
-    if (dir == kEmit)
-      hipLaunchKernelGGL((sweep_group_kernel<kEmit, 4>), grid, dim3(kBlock), shm, st, a,
-                         a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
-    else
-      hipLaunchKernelGGL((sweep_group_kernel<kAbsorb, 4>), grid, dim3(kBlock), shm, st, a,
-                         a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+  auto go = [&](auto kernel, int nw) {
+    const size_t s = sweep_shm(reinterpret_cast<const void*>(kernel), a, shm);
+    hipLaunchKernelGGL(kernel, grid, dim3(64 * nw), s, st, a, a.ssteps, a.F_up, a.F_down,
+                       a.part, a.dtaus);
+  };
+  if (NW == 8) {
+    if (Q == 4) {
+      if (dir == kEmit) go(sweep_group_kernel<kEmit, 4, 8>, 8);
+      else go(sweep_group_kernel<kAbsorb, 4, 8>, 8);
+    } else {
+      if (dir == kEmit) go(sweep_group_kernel<kEmit, 2, 8>, 8);
+      else go(sweep_group_kernel<kAbsorb, 2, 8>, 8);
+    }
+  } else if (Q == 4) {
+    if (dir == kEmit) go(sweep_group_kernel<kEmit, 4, 4>, 4);
+    else go(sweep_group_kernel<kAbsorb, 4, 4>, 4);
   } else {
-    if (dir == kEmit)
-      hipLaunchKernelGGL((sweep_group_kernel<kEmit, 2>), grid, dim3(kBlock), shm, st, a,
-                         a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
-    else
-      hipLaunchKernelGGL((sweep_group_kernel<kAbsorb, 2>), grid, dim3(kBlock), shm, st, a,
-                         a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+    if (dir == kEmit) go(sweep_group_kernel<kEmit, 2, 4>, 4);
+    else go(sweep_group_kernel<kAbsorb, 2, 4>, 4);
   }
 }
 
@@ -1270,7 +1363,7 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
   // which is not in use yet) or copied from the global step table
   FastStepS* lrec = reinterpret_cast<FastStepS*>(red + (int64_t)NC * ns * 4);
   if (a.rec_on) {
-    stage_records(a, DIR, lrec, lds);
+    (void)stage_records(a, DIR, lrec, lds);
   } else {
     const double* g = reinterpret_cast<const double*>(ss);
     double* l = reinterpret_cast<double*>(lrec);
@@ -1964,25 +2057,70 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
 // writes the next sweep's record of layer l.  Every input is loaded at the start.  The
 // convergence AND over layers rides on one arrival counter: each workgroup adds
 // 1 + 65536 * (layer not converged); the last to arrive sets iter / conv and rearms it.
-__global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a) {
+//
+// Chained (a.epoch set): the update runs as the leading workgroups of the NEXT sweep's launch
+// (sweep_chain_kernel), whose sweep blocks poll what it publishes instead of waiting for a
+// kernel boundary: each layer's new T by one write-through (sc1) store — the buffer holds
+// kPoisonT until then (the sweep that deferred this update filled it) — and the layer's
+// granule epoch[l] = (epoch_val << 2) | (run already converged << 1) | (layer converged), from
+// which every sweep block forms the convergence decision itself (the same AND over layers the
+// last-arriving workgroup makes for iter / conv), with no arrival round trip in between.
+__device__ __forceinline__ void publish_T(const UpdateArgs& a, int l, double T, int conv0,
+                                          bool c) {
+  if (a.epoch) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.T_out) + l,
+                       __builtin_bit_cast(unsigned long long, T), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.epoch + l,
+                       (a.epoch_val << 2) | (conv0 ? 2ull : 0ull) | (c ? 1ull : 0ull),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    a.T_out[l] = T;
+  }
+}
+// The convergence AND over layers (absorb with tracking: the reference's convergence test)
+// rides on one arrival counter: each of the nU workgroups adds 1 + 65536 * (layer not
+// converged); the last to arrive sets iter / conv and rearms it.
+__device__ __forceinline__ void update_arrive(const UpdateArgs& a, int nU, int it, bool nc1) {
+  if (!(a.track && a.dir == kAbsorb)) return;
+  const unsigned old = __hip_atomic_fetch_add(a.done, 1u + (nc1 ? 65536u : 0u),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((old & 0xffffu) != (unsigned)nU - 1) return;   // not the last layer in
+  const unsigned nc = (old >> 16) + (nc1 ? 1u : 0u);
+  *a.iter = it + 1;
+  if (nc == 0 && a.stop_on_conv) *a.conv = 1;
+  __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Layer lr of nU update workgroups, run by kRedThreads threads (tid) — half h of a 512-thread
+// block in a chained 8-wave launch (each half its own LDS: sh, and the [h] arrays below).  A
+// half past the last layer (lr >= n_layers, odd layer counts) computes the last layer again
+// with every side effect suppressed, so both halves meet the same block barriers.
+// sh: dynamic LDS of (2 n_layers + n_tnodes) doubles.
+__device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, int h,
+                                  double* sh) {
 #ifdef FREI_UPD_EMPTY  // diagnostic ablation build: launch floor
   return;
 #endif
   TRACE_DECL;
-  const int l = blockIdx.x;
   const int nL = a.su.n_layers;
+  const bool on = lr < nL;
+  const int l = on ? lr : nL - 1;
   const int dir = a.dir;
-  const int tid = threadIdx.x;
   const double* Tin = a.su.T;
-  extern __shared__ __attribute__((aligned(16))) double sh[];
   double* sTn = sh;                 // [nL] new T of layers l, l + 1 (the setup's T view)
   double* sP = sTn + nL;            // [nL] p of layers l, l + 1 (the setup's p view)
   double* sNodes = sP + nL;         // [n_tnodes] sorted T nodes
-  __shared__ double wsum[kRedWaves][8];
-  __shared__ double tot[8];         // this rank's sums of steps k0 (0..3) and k1 (4..7)
-  __shared__ PMeta sPm[kMaxFastS];  // layer l's metadata per species (setup)
-  __shared__ SpecMeta sSp[kMaxFastS];
-  __shared__ double sMm[kMaxFastS];
+  __shared__ double wsum_[2][kRedWaves][8];
+  __shared__ double tot_[2][8];        // this rank's sums of steps k0 (0..3) and k1 (4..7)
+  __shared__ PMeta sPm_[2][kMaxFastS];  // layer l's metadata per species (setup)
+  __shared__ SpecMeta sSp_[2][kMaxFastS];
+  __shared__ double sMm_[2][kMaxFastS];
+  auto& wsum = wsum_[h];
+  double* tot = tot_[h];
+  PMeta* sPm = sPm_[h];
+  SpecMeta* sSp = sSp_[h];
+  double* sMm = sMm_[h];
   const int k0 = layer_step(dir, l, nL);
   const int k1 = l + 1 < nL ? layer_step(dir, l + 1, nL) : -1;
   const int kn = a.next_dir >= 0 ? layer_step(a.next_dir, l, nL) : -1;
@@ -2016,7 +2154,7 @@ __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a)
   LayerPre pre{};
   if (tid < 2 && kd >= 0) pre = layer_pre(T1, T2, p1, p2, lnp, a.su.g, a.m_bar, a.alpha);
   if (!a.force && conv) {    // converged: carry T into the output buffer
-    if (tid == 0) a.T_out[l] = Tl;
+    if (tid == 0 && on) publish_T(a, l, Tl, conv, true);
     return;
   }
   // ---- this rank's sums, reduce_kernel's order (strided per thread, wave butterfly, waves)
@@ -2063,7 +2201,8 @@ __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a)
   __syncthreads();
   const long long t0 = wall_clock64();
 #ifndef FREI_P2P_NOPUSH   // diagnostic ablation build: no push (a one-rank run still completes)
-  if (a.p2p.mbox && tid == 64 && k0 >= 0) p2p_push_values(a.push, (int64_t)k0 * 4, tot, 4);
+  if (a.p2p.mbox && tid == 64 && k0 >= 0 && on)
+    p2p_push_values(a.push, (int64_t)k0 * 4, tot, 4);
 #endif
   if (tid < 64) {
     // all ranks' sums in rank order (lanes 0..7), then dT of layers l, l + 1 (lanes 0, 1)
@@ -2086,8 +2225,8 @@ __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a)
     const int base = (tid & 1) * 4;
     double F[4];
     for (int q = 0; q < 4; ++q) F[q] = __shfl(v, base + q, 64);
-    if (tid < 4 && k0 >= 0 && a.bol_out) a.bol_out[(int64_t)l * 4 + tid] = v;
-    if (tid == 0 && l == 0 && a.p2p.mbox && a.p2p.wait_ticks)
+    if (tid < 4 && k0 >= 0 && a.bol_out && on) a.bol_out[(int64_t)l * 4 + tid] = v;
+    if (tid == 0 && lr == 0 && a.p2p.mbox && a.p2p.wait_ticks)
       atomicAdd(a.p2p.wait_ticks, (unsigned long long)(wall_clock64() - t0));
     double d = 0.0;
     if (tid < 2 && kd >= 0) {
@@ -2098,7 +2237,7 @@ __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a)
 #endif
       sTn[li] = T1 - d;
     }
-    if (tid == 0) {
+    if (tid == 0 && on) {
       // layer l's bookkeeping (update_kernel's expressions)
       const double dT = d;
       const double Tnew = Tl - dT;
@@ -2127,33 +2266,85 @@ __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a)
           c = (flips > a.n_zero_crossings) || (fabs(dT) < a.convergence_dT);
         }
       }
-      a.T_out[l] = Tnew;
+      publish_T(a, l, Tnew, conv, c);
       if (kd < 0) sTn[l] = Tnew;
-      if (a.track && dir == kAbsorb) {
-        const unsigned old = __hip_atomic_fetch_add(a.done, 1u + (c ? 0u : 65536u),
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((old & 0xffffu) == gridDim.x - 1) {   // last layer in: every other one has counted
-          const unsigned nc = (old >> 16) + (c ? 0u : 1u);
-          *a.iter = it + 1;
-          if (nc == 0 && a.stop_on_conv) *a.conv = 1;
-          __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
+      update_arrive(a, nU, it, !c);
     }
   }
   TRACE_MARK(2);
   __syncthreads();   // sTn of layers l, l + 1
 #ifndef FREI_UPD_NOSETUP  // diagnostic ablation build
-  if (kn >= 0 && tid >= 64) {
+  if (kn >= 0 && tid >= 64 && on) {
     if (stage)
       setup_sweep(a.su, sTn, sP, sNodes, sSp, sPm, sMm, a.next_dir, kn, kn + 1, tid - 64,
-                  blockDim.x - 64, 1, l);
+                  kRedThreads - 64, 1, l);
     else
       setup_sweep(a.su, sTn, sP, sNodes, a.su.spec, a.su.pmeta, a.su.mmr, a.next_dir, kn,
-                  kn + 1, tid - 64, blockDim.x - 64, nL, 0);
+                  kn + 1, tid - 64, kRedThreads - 64, nL, 0);
   }
 #endif
   TRACE_PUT(30);
+}
+
+__global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double sh[];
+  update_fused_body(a, blockIdx.x, gridDim.x, threadIdx.x, 0, sh);
+}
+
+// Chained launch: workgroups [0, nU) run the previous sweep's fused update (u; with 8-wave
+// blocks each workgroup's two 256-thread halves take a layer each), the rest sweep.  One
+// atmosphere.  Forward progress: the update workgroups wait for nothing in this launch (only
+// for the other ranks' sums, over P2P), so the sweep blocks' bounded polls always end.
+template <int DIR, int Q, int NW>
+__global__ __launch_bounds__(64 * NW) void sweep_chain_kernel(
+    FastArgs a, UpdateArgs u, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
+    double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
+  static_assert(kRedThreads == 256, "update halves of 256 threads");
+  extern __shared__ double red[];
+  const int nL = u.su.n_layers;
+  constexpr int kHalves = NW / 4;
+  const int nU = (nL + kHalves - 1) / kHalves;
+  if ((int)blockIdx.x < nU) {
+    const int h = threadIdx.x >> 8;
+    update_fused_body(u, blockIdx.x * kHalves + h, nL, threadIdx.x & 255, h,
+                      red + (int64_t)h * (2 * nL + u.su.n_tnodes));
+    return;
+  }
+  sweep_group_body<DIR, Q, NW, true>(a, ss, Fu, Fd, part, dtaus, red, blockIdx.x - nU,
+                                     gridDim.x - nU);
+}
+
+// The chained launch of a grouped-lane sweep: the update workgroups of u ahead of nblocks sweep
+// blocks, dynamic LDS for the larger of the two.
+void launch_sweep_chain(int dir, int Q, int NW, const FastArgs& a, const UpdateArgs& u,
+                        int nblocks, hipStream_t st) {
+  const int nL = u.su.n_layers;
+  const int nU = (nL + NW / 4 - 1) / (NW / 4);
+  size_t shm = (size_t)red_lds_doubles(a.red_rows, a.n_steps, NW) * sizeof(double) +
+               (size_t)a.n_steps * sizeof(FastStepS) +
+               (size_t)rec_scratch_doubles(a) * sizeof(double);
+  const size_t ushm = (size_t)(NW / 4) * (2 * nL + u.su.n_tnodes) * sizeof(double);
+  if (ushm > shm) shm = ushm;
+  auto go = [&](auto kernel) {
+    const size_t s = sweep_shm(reinterpret_cast<const void*>(kernel), a, shm);
+    hipLaunchKernelGGL(kernel, dim3(nU + nblocks), dim3(64 * NW), s, st, a, u, a.ssteps,
+                       a.F_up, a.F_down, a.part, a.dtaus);
+  };
+  if (NW == 8) {
+    if (Q == 4) {
+      if (dir == kEmit) go(sweep_chain_kernel<kEmit, 4, 8>);
+      else go(sweep_chain_kernel<kAbsorb, 4, 8>);
+    } else {
+      if (dir == kEmit) go(sweep_chain_kernel<kEmit, 2, 8>);
+      else go(sweep_chain_kernel<kAbsorb, 2, 8>);
+    }
+  } else if (Q == 4) {
+    if (dir == kEmit) go(sweep_chain_kernel<kEmit, 4, 4>);
+    else go(sweep_chain_kernel<kAbsorb, 4, 4>);
+  } else {
+    if (dir == kEmit) go(sweep_chain_kernel<kEmit, 2, 4>);
+    else go(sweep_chain_kernel<kAbsorb, 2, 4>);
+  }
 }
 
 // ---------------------------------------------------------------- standalone kernels
@@ -2609,9 +2800,10 @@ static void launch_fast_t(const FastArgs& a, int nblocks, hipStream_t st) {
                      (SH ? (size_t)a.n_steps * sizeof(FastStepS) +
                                (size_t)rec_scratch_doubles(a) * sizeof(double)
                          : 0);
-  hipLaunchKernelGGL((sweep_fast_kernel<DIR, S, PD, NC, SH, MM1, PF>),
-                     dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1), dim3(kBlock), shm,
-                     st, a, a.steps, a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+  const auto kernel = sweep_fast_kernel<DIR, S, PD, NC, SH, MM1, PF>;
+  hipLaunchKernelGGL(kernel, dim3(nblocks, a.n_atm > 1 ? a.n_atm : 1), dim3(kBlock),
+                     sweep_shm(reinterpret_cast<const void*>(kernel), a, shm), st, a, a.steps,
+                     a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
 }
 
 // the contracted one-table sweep (S = 1, unit mmr) with prefetch distance pf (0: = PD)

@@ -112,7 +112,16 @@ struct frei_ctx {
   // the fused reduce + update writes the new temperatures into the other buffer and the two
   // swap (d_T is always the current one); d_done: its arrival counter
   double* d_T_alt = nullptr;
+  double* d_T3 = nullptr;               // third temperature buffer (chained launches)
   double* d_T_home = nullptr;           // the buffer d_T names after a host upload
+  // Chained launches (FREI_CHAIN): a sweep's fused update is deferred and runs as the leading
+  // workgroups of the next sweep's launch (launch_sweep_chain)
+  int chain = 0;                        // FREI_CHAIN
+  bool has_pend = false;                // an update deferred to the next launch
+  UpdateArgs pend{};
+  unsigned long long* d_epoch = nullptr;  // [n_layers] the chained update's per-layer granules
+  unsigned long long chain_seq = 0;
+  int* d_chain_err = nullptr;           // a chained sweep block's wait gave up
   unsigned* d_done = nullptr;
   int fused_update = 1;                 // FREI_FUSED_UPDATE=0: separate reduce and update kernels
   // T-P iterations replayed from a captured hipGraph (frei_iterate / frei_run, timing off,
@@ -207,6 +216,8 @@ struct frei_ctx {
   int pipe_pf = 1;                      // FREI_PIPE_PF: phases the producers load ahead (1, 2)
   int red_rows = 1;                     // FREI_RED_ROWS=0: full wave sums per step
   int red_stage = 1;                    // FREI_RED_STAGE=0: no staged sums (one-lane sweep)
+  int sweep_lds_kb = 0;                 // FREI_SWEEP_LDS_KB: minimum LDS per sweep block (KiB)
+  int group_waves = 4;                  // FREI_GROUP_WAVES: waves per grouped-lane sweep block
   int depth4_max_blocks = 0;            // FREI_DEPTH4_MAX_BLOCKS (4 steps in flight: off, measured no faster)
   size_t lds_per_block = 64 * 1024;     // hipDeviceProp sharedMemPerBlock
   size_t lds_optin = 64 * 1024;         // with the dynamic-LDS opt-in (gfx950: 160 KiB)
@@ -612,6 +623,46 @@ struct SweepOpts {
   int live_only = 0;          // T-P loop: skip stores no later sweep reads
 };
 
+// Temperature buffers: d_T is the current one; an update writes a buffer that is neither d_T
+// (its input) nor `busy` (the input of an update still running in the same launch), which
+// then becomes d_T.
+void rotate_T(frei_ctx* c, double* out) {
+  double* b[3] = {c->d_T, c->d_T_alt, c->d_T3};
+  double* rest[2];
+  int n = 0;
+  for (double* x : b)
+    if (x != out && n < 2) rest[n++] = x;
+  c->d_T = out;
+  c->d_T_alt = rest[0];
+  c->d_T3 = rest[1];
+}
+double* free_T(frei_ctx* c, const double* busy) { return c->d_T_alt != busy ? c->d_T_alt : c->d_T3; }
+
+// reduce + update fused into one launch: one atmosphere, exchange local or P2P (RCCL and the
+// host hook need the rank's sums in memory between the two kernels)
+bool fused_ok(frei_ctx* c) {
+  return c->fused_update && c->n_atm == 1 && !c->comm && !(c->nranks > 1 && c->host_ag) &&
+         (2 * (size_t)c->nL + c->tnodes.size()) * sizeof(double) <= 32 * 1024;
+}
+
+// This sweep can run chained: the grouped-lane sweep forming its own records, fused update,
+// stream launches (no graph capture).
+bool chain_ready(frei_ctx* c) {
+  return c->chain && c->fast && c->eff && c->shared && records_in_sweep(c) &&
+         group_lanes(c) > 1 && pipe_consumers(c) == 0 && fused_ok(c) && !c->use_graph &&
+         !c->keys;
+}
+
+// Launch a deferred update on its own (the next sweep cannot take it, or the caller needs its
+// results now).  Its output buffer holds kPoisonT until the update writes it.
+int flush_update(frei_ctx* c) {
+  if (!c->has_pend) return 0;
+  c->has_pend = false;
+  launch_update_fused(c->pend, c->stream);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 // FNV-1a over an argument block (zero-initialised structs: padding bytes are zero)
 template <typename T>
 uint64_t arg_hash(uint64_t h, const T& x) {
@@ -625,8 +676,16 @@ uint64_t arg_hash(uint64_t h, const T& x) {
 // fused_update 0).  Asynchronous.
 // With c->dry it only appends the hash of every launch's arguments to c->keys and applies
 // the host-side state changes (temperature buffer swap), launching nothing.
-int run_sweep(frei_ctx* c, const SweepOpts& o) {
+int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
   const int ns = c->nL - 1;
+  // chained: this sweep's launch also runs the deferred update (merge), and this sweep's own
+  // update may be deferred to the next launch (defer_own)
+  const bool chain = !c->dry && chain_ready(c);
+  if (c->has_pend && !chain) TRY(flush_update(c));
+  const bool merge = chain && c->has_pend;
+  const bool defer_own = chain && defer;
+  // the output buffer of this sweep's update: not d_T, and not the merged update's input
+  double* T_next = chain ? free_T(c, merge ? c->pend.su.T : nullptr) : c->d_T_alt;
   SweepArgs a{};
   a.n_lam = c->nlam;
   a.n_steps = ns;
@@ -687,6 +746,15 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     f.n_atm = c->n_atm;
     f.unit_mmr = c->eff ? 1 : 0;
     f.rec_on = rec_on ? 1 : 0;
+    f.min_lds = c->sweep_lds_kb * 1024;
+    if (merge) {   // this launch's leading workgroups run the deferred update
+      f.ch_epoch = c->d_epoch;
+      f.ch_val = ++c->chain_seq;
+      f.ch_can_conv = c->pend.track && c->pend.dir == kAbsorb && c->pend.stop_on_conv;
+      f.ch_timeout = (long long)(c->p2p_timeout_s * 1e8);   // wall_clock64: 100 MHz
+      f.ch_err = c->d_chain_err;
+    }
+    if (defer_own) f.poison = T_next;
     if (f.rec_on) f.rec = setup_args(c);   // T of this sweep: c->d_T now
     // per-row partials while the one-lane sweep's LDS stays within 48 KiB (3+ blocks per CU)
     f.red_rows = c->red_rows &&
@@ -709,20 +777,27 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
         ((size_t)(kBlock / 64) * ns * 4 + (size_t)(kBlock / 64) * 2 * 4 * 72) * sizeof(double) +
                 (size_t)ns * sizeof(FastStepS) <= 48 * 1024)
       f.red_rows = 2;
-    if (Q > 1) nb_run = (int)((c->nlam + kBlock / Q - 1) / (kBlock / Q));
+    const int NW = c->group_waves;
+    if (Q > 1) nb_run = (int)((c->nlam + 64 * NW / Q - 1) / (64 * NW / Q));
     const int NC = pipe_consumers(c);
     if (NC > 0) nb_run = (int)((c->nlam + 64 * NC - 1) / (64 * NC));
     if (c->keys) {
       uint64_t h = arg_hash(1469598103934665603ull, f);
-      const int cfg[9] = {o.dir, Q, S_run, depth, (nan_check && !c->eff) ? 1 : 0, c->shared,
-                          NC, c->pipe_pf, pf};
+      const int cfg[10] = {o.dir, Q, S_run, depth, (nan_check && !c->eff) ? 1 : 0, c->shared,
+                           NC, c->pipe_pf, pf, NW};
       c->keys->push_back(arg_hash(h, cfg));
     }
     if (c->dry) {
     } else if (NC > 0) {
       launch_sweep_pipe(o.dir, NC, c->pipe_pf, f, nb_run, c->stream);
+    } else if (Q > 1 && merge) {
+      UpdateArgs u = c->pend;
+      u.epoch = c->d_epoch;
+      u.epoch_val = c->chain_seq;
+      c->has_pend = false;
+      launch_sweep_chain(o.dir, Q, NW, f, u, nb_run, c->stream);
     } else if (Q > 1) {
-      launch_sweep_group(o.dir, Q, f, nb_run, c->stream);
+      launch_sweep_group(o.dir, Q, NW, f, nb_run, c->stream);
     } else {
       launch_sweep_fast(o.dir, S_run, depth, pf, nan_check && !c->eff, c->shared != 0, f,
                         c->nblocks, c->stream);
@@ -752,9 +827,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
   }
   // one launch for reduce + update: one atmosphere, exchange local or P2P (RCCL and the host
   // hook need the rank's sums in memory between the two kernels)
-  const bool fused = c->fused_update && c->n_atm == 1 && !c->comm &&
-                     !(c->nranks > 1 && c->host_ag) &&
-                     (2 * (size_t)c->nL + c->tnodes.size()) * sizeof(double) <= 32 * 1024;
+  const bool fused = fused_ok(c);
   if (!fused && c->dry) {   // not graph-replayable (the check in iterate() sees the marker)
     if (c->keys) c->keys->push_back(0);
     return 0;
@@ -832,12 +905,17 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
     u.part = c->d_part;
     u.nblocks = nb_run;
     u.push = push;
-    u.T_out = c->d_T_alt;
+    u.T_out = T_next;
     u.done = c->d_done;
     if (c->keys) c->keys->push_back(arg_hash(1469598103934665603ull, u));
-    if (!c->dry) launch_update_fused(u, c->stream);
+    if (defer_own) {   // runs at the head of the next sweep's launch, or flush_update
+      c->pend = u;
+      c->has_pend = true;
+    } else if (!c->dry) {
+      launch_update_fused(u, c->stream);
+    }
     HIP_TRY(hipGetLastError());
-    std::swap(c->d_T, c->d_T_alt);
+    rotate_T(c, T_next);
     return 0;
   }
   launch_update(u, c->stream, c->n_atm);
@@ -848,7 +926,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o) {
 // A host upload overwrites the current temperatures, so the fused update's ping-pong can
 // restart from the same buffer (every run then issues identical launch arguments).
 void home_temperatures(frei_ctx* c) {
-  if (c->d_T != c->d_T_home) std::swap(c->d_T, c->d_T_alt);
+  if (c->d_T != c->d_T_home) rotate_T(c, c->d_T_home);
 }
 
 int reset_loop_state(frei_ctx* c) {
@@ -902,7 +980,8 @@ const char* const kOptionNames[] = {"prefetch_depth", "shared", "shared_max_bloc
                                     "precontract", "depth4_max_blocks", "pair_max_blocks",
                                     "quad_max_blocks", "red_rows", "red_stage", "group_q",
                                     "fused_update", "graph", "pipe", "pipe_pf", "pipe_min_blocks", "rec_sweep",
-                                    "pipe_max_blocks", "prefetch_steps", "k7_mfma", nullptr};
+                                    "pipe_max_blocks", "prefetch_steps", "k7_mfma", "sweep_lds_kb", "group_waves", "chain",
+                                    nullptr};
 int set_option(frei_ctx* c, const std::string& k, int v) {
   if (k == "prefetch_depth") c->prefetch_depth = v;
   else if (k == "shared") c->shared_mode = v < 0 ? -1 : (v ? 1 : 0);
@@ -922,6 +1001,9 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "pipe_max_blocks") c->pipe_max_blocks = v;
   else if (k == "pipe_pf") c->pipe_pf = v == 1 ? 1 : 2;
   else if (k == "k7_mfma") c->k7_mfma = v != 0;
+  else if (k == "group_waves") c->group_waves = v == 8 ? 8 : 4;
+  else if (k == "chain") c->chain = v != 0;
+  else if (k == "sweep_lds_kb") c->sweep_lds_kb = v < 0 ? 0 : (v > 160 ? 160 : v);
   else if (k == "prefetch_steps") c->prefetch_steps = v >= 16 ? 16 : v >= 8 ? 8 : 0;
   else return fail("unknown option '" + k + "'");
   c->meta_dirty = true;
@@ -930,6 +1012,11 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
 
 // After a stream synchronize: did a P2P wait time out (a rank never published its sums)?
 int check_comm(frei_ctx* c) {
+  if (c->d_chain_err) {
+    int e = 0;
+    HIP_TRY(hipMemcpy(&e, c->d_chain_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (e) return fail("chained sweep: the update workgroups never published the temperatures");
+  }
   if (!c->d_comm_err) return 0;
   int e = 0;
   HIP_TRY(hipMemcpy(&e, c->d_comm_err, sizeof(int), hipMemcpyDeviceToHost));
@@ -1000,6 +1087,8 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
       (rc = dalloc(&c->d_wtr, n_lam)) || (rc = dalloc(&c->d_p, NL)) || (rc = dalloc(&c->d_lnp, NL)) ||
       (rc = dalloc(&c->d_Fu, F)) || (rc = dalloc(&c->d_Fd, F)) ||
       (rc = dalloc(&c->d_T, NL * A)) || (rc = dalloc(&c->d_T_alt, NL * A)) ||
+      (rc = dalloc(&c->d_T3, NL * A)) || (rc = dalloc(&c->d_epoch, NL)) ||
+      (rc = dalloc(&c->d_chain_err, 1)) ||
       (rc = dalloc(&c->d_done, 1)) || (rc = dalloc(&c->d_dT, NL * A)) ||
       (rc = dalloc(&c->d_bol, NL * 4 * A)) || (rc = dalloc(&c->d_mmr, NS * NL * A)) ||
       (rc = dalloc(&c->d_steps, ns * A)) || (rc = dalloc(&c->d_terms, ns * NS * A)) ||
@@ -1022,6 +1111,8 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
       hipMemsetAsync(c->d_Fd, 0, F * sizeof(double), c->stream) != hipSuccess ||
       hipMemsetAsync(c->d_conv, 0, sizeof(int) * A, c->stream) != hipSuccess ||
       hipMemsetAsync(c->d_done, 0, sizeof(unsigned), c->stream) != hipSuccess ||
+      hipMemsetAsync(c->d_epoch, 0, sizeof(unsigned long long) * NL, c->stream) != hipSuccess ||
+      hipMemsetAsync(c->d_chain_err, 0, sizeof(int), c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return bail(fail("hipMemsetAsync failed"));
   if (A > 1 && hipHostMalloc((void**)&c->h_conv, 2 * A * sizeof(int)) != hipSuccess)
@@ -1055,6 +1146,8 @@ int frei_ctx_destroy(frei_ctx* c) {
   dfree(c->d_mbox);
   dfree(c->d_comm_err);
   dfree(c->d_wait_ticks);
+  dfree(c->d_epoch);
+  dfree(c->d_chain_err);
   for (auto& s : c->sp) dfree(s.d_tab);
   dfree(c->d_eff);
   dfree(c->d_smeta_eff);
@@ -1065,7 +1158,7 @@ int frei_ctx_destroy(frei_ctx* c) {
   dfree(c->d_ones);
   dfree(c->d_prow);
   double* dd[] = {c->d_c1, c->d_hcl, c->d_sig, c->d_ftoa, c->d_wtr, c->d_p, c->d_lnp,
-                  c->d_Fu, c->d_Fd, c->d_T, c->d_T_alt, c->d_dT, c->d_dtaus, c->d_bol, c->d_tnodes, c->d_mmr, c->d_part,
+                  c->d_Fu, c->d_Fd, c->d_T, c->d_T_alt, c->d_T3, c->d_dT, c->d_dtaus, c->d_bol, c->d_tnodes, c->d_mmr, c->d_part,
                   c->d_Fb, c->d_Fb_all, c->d_Tb, c->d_Ta, c->d_hist};
   for (double* p : dd)
     if (p) (void)hipFree(p);
@@ -1434,16 +1527,16 @@ static int iterate_direct(frei_ctx* c, int n, int nzc, double thr, double alpha,
     e.track = 1;
     e.alpha = alpha;
     e.live_only = 1;
-    TRY(run_sweep(c, e));
+    TRY(run_sweep(c, e, true));
     SweepOpts a = e;
     a.dir = kAbsorb;
     a.next_dir = kEmit;
     a.stop_on_conv = stop ? 1 : 0;
     a.n_zero_crossings = nzc;
     a.convergence_dT = thr;
-    TRY(run_sweep(c, a));
+    TRY(run_sweep(c, a, true));
   }
-  return 0;
+  return flush_update(c);   // no call returns with an update still deferred
 }
 
 // Graph replay applies when one iteration is two fused launches pairs on one rank with no

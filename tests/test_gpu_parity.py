@@ -498,13 +498,14 @@ def test_species_contraction_matches_per_species_sum(fa, monkeypatch):
                            T=out[mode]["final_T"], ref_T=oT)
 
 
+@pytest.mark.parametrize("waves", [4, 8])          # waves per block (8: two per SIMD, lockstep)
 @pytest.mark.parametrize("red_mode", ["stage", "rows", "full"])   # partial-sum layouts
 @pytest.mark.parametrize("n_layers", [34, 36])     # 33 / 35 steps: dummy group slots
-def test_grouped_lane_sweep_matches_one_lane_form(fa, monkeypatch, n_layers, red_mode):
-    """The grouped-lane sweeps (two or four lanes per wavelength, small slices) form every
-    flux with the one-lane expressions: one sweep from the same state gives bit-identical
-    fluxes and dtaus; only the bolometric partial sums use another fixed summation tree (dT
-    within 1e-10), so T-P iterations agree within the parity tolerance."""
+def test_grouped_lane_sweep_matches_one_lane_form(fa, monkeypatch, n_layers, red_mode, waves):
+    """The grouped-lane sweeps (two or four lanes per wavelength, small slices; 4- or 8-wave
+    blocks) form every flux with the one-lane expressions: one sweep from the same state gives
+    bit-identical fluxes and dtaus; only the bolometric partial sums use another fixed summation
+    tree (dT within 1e-10), so T-P iterations agree within the parity tolerance."""
     rng = np.random.default_rng(9)
     lam, _, _ = O.wavelength_grid(0.5, 10, 5000)
     p = O.pressure_grid(n_layers, -6, np.log10(200))
@@ -517,6 +518,7 @@ def test_grouped_lane_sweep_matches_one_lane_form(fa, monkeypatch, n_layers, red
     out = {}
     monkeypatch.setenv("FREI_RED_STAGE", "1" if red_mode == "stage" else "0")
     monkeypatch.setenv("FREI_RED_ROWS", "1" if red_mode == "rows" else "0")
+    monkeypatch.setenv("FREI_GROUP_WAVES", str(waves))
     for q in (4, 2, 1):
         monkeypatch.setenv("FREI_GROUP_Q", str(q))
         eng = fa.Engine(lam, p, tabs, mmr=mmr)

@@ -22,7 +22,44 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 KIND = {1: "sweep_fast", 12: "sweep_group2", 14: "sweep_group4", 21: "sweep_pipe1",
-        22: "sweep_pipe2", 24: "sweep_pipe4", 30: "update_fused", 40: "sweep_upd"}
+        22: "sweep_pipe2", 24: "sweep_pipe4", 30: "update_fused", 42: "chain_group2",
+        44: "chain_group4"}
+
+
+def chained(rec, tick):
+    """Launches by time overlap (a chained launch holds update and sweep blocks): per kind, the
+    medians over launches of the first entry, median prologue end, last loop end and last exit,
+    all relative to the launch's first entry."""
+    rec = rec[np.argsort(rec[:, 2], kind="stable")]
+    cl, cur_end = [], None
+    for r in rec:
+        if cur_end is None or r[2] > cur_end:
+            cl.append([])
+            cur_end = r[5]
+        cl[-1].append(r)
+        cur_end = max(cur_end, r[5])
+    by = {}
+    for i, c in enumerate(cl):
+        a = np.array(c)
+        t0 = a[:, 2].min()
+        key = tuple(sorted({int(k) for k in a[:, 0]}))
+        row = {}
+        for k in key:
+            b = a[a[:, 0] == k]
+            row[k] = ((b[:, 2].min() - t0) * tick, (np.median(b[:, 3]) - t0) * tick,
+                      (b[:, 4].max() - t0) * tick, (b[:, 5].max() - t0) * tick)
+        gap = (t0 - cl[i - 1][-1][5]) * tick if i else None
+        prev_end = max(x[5] for x in cl[i - 1]) if i else None
+        by.setdefault(key, []).append((row, (t0 - prev_end) * tick if i else None,
+                                       (a[:, 5].max() - t0) * tick))
+    for key, rows in by.items():
+        print(f"launch type {[KIND.get(k, k) for k in key]}: {len(rows)} launches; median gap from "
+              f"previous launch {np.median([g for _, g, _ in rows if g is not None]):.2f} us, "
+              f"span {np.median([s for _, _, s in rows]):.2f} us")
+        for k in key:
+            v = np.median(np.array([r[k] for r, _, _ in rows]), axis=0)
+            print(f"   {KIND.get(k, k):>14s}: first entry {v[0]:6.2f}  median prologue end {v[1]:6.2f}"
+                  f"  last loop end {v[2]:6.2f}  last exit {v[3]:6.2f}")
 
 
 def launches(rec):
@@ -94,8 +131,14 @@ def main():
     if n.value > cap:
         print(f"trace overflow: {n.value} records > {cap}")
     rec = buf[:min(n.value, cap)].copy()
-    Ls = launches(rec)
     tick = 0.01   # us per wall_clock64 tick (100 MHz)
+    if any(int(k) >= 40 for k in rec[:, 0]):
+        print(f"slice {a.slice}  n_lam {a.n_lam}  p2p {a.p2p}  {a.iters} T-P iterations: "
+              f"{wall * 1e3:.2f} us each (wall, no profiler)")
+        chained(rec, tick)
+        eng.close()
+        return
+    Ls = launches(rec)
     for i in range(1, len(Ls)):
         Ls[i]["gap"] = (Ls[i]["start"] - Ls[i - 1]["end"]) * tick
     Ls[0]["gap"] = None
