@@ -384,7 +384,10 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
 #define FREI_WT_STORE 0
 #endif
 __device__ __forceinline__ void flux_store(double* p, double v) {
-#if FREI_WT_STORE
+#if FREI_WT_STORE == 2   // agent scope: global_store sc1 (write-through to memory, line dropped)
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif FREI_WT_STORE
   __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v),
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #else
@@ -576,16 +579,25 @@ __device__ __forceinline__ int stage_records(const FastArgs& a, int dir, FastSte
   double* sP = sT + nL;
   double* sN = sP + nL;
   int skip = 0, allc = 1;   // chained: run already converged / every layer converged
-  for (int q = tid; q < nL; q += nthr) {
-    if (a.ch_epoch) {
+  if (a.ch_epoch) {
+    // ONE lane polls (the update workgroups publish within about a microsecond of each other;
+    // every lane polling would put hundreds of thousands of loads in flight on the same few
+    // lines and slow the update itself), then every lane reads its layers once — polling on
+    // only for a value not yet there
+    if (tid == 0) (void)chain_poll(a, a.ch_epoch + (nL - 1), 0, a.ch_val, true);
+    __syncthreads();
+    for (int q = tid; q < nL; q += nthr) {
       sT[q] = __builtin_bit_cast(double, chain_poll(a, u.T + q, kPoisonT, 0, false));
       const unsigned long long g = chain_poll(a, a.ch_epoch + q, 0, a.ch_val, true);
       skip |= (int)((g >> 1) & 1);
       allc &= (int)(g & 1);
-    } else {
-      sT[q] = u.T[q];
+      sP[q] = u.p[q];
     }
-    sP[q] = u.p[q];
+  } else {
+    for (int q = tid; q < nL; q += nthr) {
+      sT[q] = u.T[q];
+      sP[q] = u.p[q];
+    }
   }
   for (int q = tid; q < ntn; q += nthr) sN[q] = u.tnodes[q];
   // this thread's first record's metadata, loaded with T / p (one global round trip in all)
@@ -594,6 +606,7 @@ __device__ __forceinline__ int stage_records(const FastArgs& a, int dir, FastSte
   if (a.ch_epoch) {
     // the update's convergence decision, formed from its per-layer granules: the sweep does
     // not run once the run has converged (as an unchained sweep returns at entry)
+    // (logical block reductions: __syncthreads_or / _and return 0 or 1, not bit patterns)
     skip = __syncthreads_or(skip);
     allc = __syncthreads_and(allc);
     if ((skip || (a.ch_can_conv && allc)) && !a.force) return 1;

@@ -116,7 +116,7 @@ struct frei_ctx {
   double* d_T_home = nullptr;           // the buffer d_T names after a host upload
   // Chained launches (FREI_CHAIN): a sweep's fused update is deferred and runs as the leading
   // workgroups of the next sweep's launch (launch_sweep_chain)
-  int chain = 0;                        // FREI_CHAIN
+  int chain = 1;                        // FREI_CHAIN
   bool has_pend = false;                // an update deferred to the next launch
   UpdateArgs pend{};
   unsigned long long* d_epoch = nullptr;  // [n_layers] the chained update's per-layer granules
