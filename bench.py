@@ -380,6 +380,10 @@ def main():
         # ranks' update kernels spinning on the same GPU for their peers' sums its blocks can
         # starve (a P2P timeout): ranks that share a GPU use the grouped-lane form instead
         os.environ.setdefault("FREI_PIPE", "0")
+        # likewise a chained launch's sweep blocks wait (spinning) for its update workgroups,
+        # which wait for every rank's sums: beside other ranks' kernels on the same GPU they could
+        # hold the CUs those ranks need, so ranks sharing a GPU launch update and sweep separately
+        os.environ.setdefault("FREI_CHAIN", "0")
     w = c3(n_layers=a.n_layers, n_lam=a.n_lam, n_T=a.n_T)
     nL, n_lam, S = a.n_layers, a.n_lam, len(w["names"])
     lo, hi = partition(n_lam, d.world, d.rank)
