@@ -114,6 +114,21 @@ def main():
         kw["lam_slice"] = partition(a.n_lam, nr, r)
     eng = Engine(w["lam"], w["p"], tabs, mmr=w["mmr"], device=0, comm=comm, **kw)
     L = N.lib()
+    if not hasattr(L, "frei_trace_fetch"):   # a production build: the wall-clock rate only
+        eng.state_init(w["T0"])
+        eng.iterate(a.warmup)
+        eng.synchronize()
+        walls = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            eng.iterate(a.iters)
+            eng.synchronize()
+            walls.append((time.perf_counter() - t0) / a.iters * 1e3)
+        print(f"slice {a.slice} {kw.get('lam_slice')}  n_lam {a.n_lam}  p2p {a.p2p}: "
+              f"{np.median(walls) * 1e3:.2f} us per T-P iteration (median of 5 x {a.iters}; "
+              f"min {min(walls) * 1e3:.2f})")
+        eng.close()
+        return
     fetch = L.frei_trace_fetch
     fetch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     cap = 1 << 17
