@@ -629,11 +629,12 @@ __device__ __forceinline__ int stage_records(const FastArgs& a, int dir, FastSte
 // loads of step k + PF are issued while step k computes, into a register ring of PF entries
 // (the step loop is unrolled by PF, so every ring index is static).  PF > PD pays on small
 // slices, where about one wave per SIMD cannot hide HBM latency with PD steps of loads alone.
-template <int DIR, int S, int PD, bool NANCHK, bool SH, bool MM1, int PF>
-__global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
-    FastArgs a, const FastStep* __restrict__ st, const FastStepS* __restrict__ ss,
+template <int DIR, int S, int PD, bool NANCHK, bool SH, bool MM1, int PF, bool CH>
+__device__ __forceinline__ void sweep_fast_body(
+    FastArgs& a, const FastStep* __restrict__ st, const FastStepS* __restrict__ ss,
     double* __restrict__ Fu, double* __restrict__ Fd, double* __restrict__ part,
-    double* __restrict__ dtaus) {
+    double* __restrict__ dtaus, double* red, const int bx, const int nbx) {
+  static_assert(!CH || SH, "chained: the step records are formed in the block (LDS)");
   static_assert(PD == 1 || PD == 2 || PD == 4, "prefetch depth 1, 2 or 4");
   static_assert(PF % PD == 0, "prefetch distance: a multiple of the coefficient block");
   static_assert(!MM1 || S == 1, "mmr = 1 only for the contracted single table");
@@ -653,14 +654,17 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     a.ftoa += m * a.bs.ftoa;
     a.conv += m;
   }
-  if (!a.force && *a.conv) return;
+  if (!CH && !a.force && *a.conv) return;
   TRACE_DECL;
-  extern __shared__ double red[];  // [wave][step][4], then (shared brackets) the step table
+  // red: [wave][step][4], then (shared brackets) the step table
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
   const int64_t nl = a.n_lam;
-  const int64_t j0 = (int64_t)blockIdx.x * kBlock + tid;
+  if (a.poison && bx == 0)   // the deferred update's output temperatures: "not published"
+    for (int i = tid; i <= a.n_steps; i += kBlock)
+      reinterpret_cast<unsigned long long*>(a.poison)[i] = kPoisonT;
+  const int64_t j0 = (int64_t)bx * kBlock + tid;
   const bool act = j0 < nl;
   const int64_t j = act ? j0 : nl - 1;
   const double c1 = a.c1[j], hcl = a.hcl[j], sig = a.sig[j];
@@ -675,7 +679,7 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     double* lss = red + red_lds_doubles(a.red_rows, ns);
     constexpr int kW = sizeof(FastStepS) / sizeof(double);
     if (a.rec_on) {   // form the records here from the current T (the update wrote none)
-      (void)stage_records(a, DIR, reinterpret_cast<FastStepS*>(lss), lss + ns * kW);
+      if (stage_records(a, DIR, reinterpret_cast<FastStepS*>(lss), lss + ns * kW)) return;
     } else {
       const double* g = reinterpret_cast<const double*>(ss);
       for (int idx = tid; idx < ns * kW; idx += kBlock) lss[idx] = g[idx];
@@ -939,9 +943,19 @@ __global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
     double s = red[idx];
     for (int w = 1; w < red_rows_per_block(a.red_rows); ++w)
       s += red[(int64_t)w * ns * 4 + idx];
-    part[(int64_t)idx * gridDim.x + blockIdx.x] = s;
+    part[(int64_t)idx * nbx + bx] = s;
   }
-  TRACE_PUT(1);
+  TRACE_PUT(CH ? 41 : 1);
+}
+
+template <int DIR, int S, int PD, bool NANCHK, bool SH, bool MM1, int PF>
+__global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
+    FastArgs a, const FastStep* __restrict__ st, const FastStepS* __restrict__ ss,
+    double* __restrict__ Fu, double* __restrict__ Fd, double* __restrict__ part,
+    double* __restrict__ dtaus) {
+  extern __shared__ double red[];
+  sweep_fast_body<DIR, S, PD, NANCHK, SH, MM1, PF, false>(a, st, ss, Fu, Fd, part, dtaus, red,
+                                                         blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------- K1, grouped-lane form
@@ -1359,9 +1373,20 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int sub = wv >> 2;    // 64-wavelength chunk of the block
-  // 0 .. 2: producer, 3: consumer (rotating the consumer across the chunks measured 3-5 %
-  // slower at 62.5k wavelengths)
-  const int role = wv & 3;
+  // 0 .. 2: producer, 3: consumer.  Waves w and w + 4 share a SIMD (profiles/r03/simd_map.txt),
+  // so role = w & 3 puts all four consumers on one SIMD and the producers' work on the other
+  // three; FREI_PIPE_ROT rotates the roles per chunk (every SIMD: three producers and one
+  // consumer), FREI_PIPE_PRIO raises the consumer's issue priority (its chain paces the phase).
+#ifndef FREI_PIPE_ROT
+#define FREI_PIPE_ROT 0
+#endif
+#ifndef FREI_PIPE_PRIO
+#define FREI_PIPE_PRIO 0
+#endif
+  const int role = FREI_PIPE_ROT ? ((wv + sub) & 3) : (wv & 3);
+#if FREI_PIPE_PRIO
+  if (role == kPipeP) __builtin_amdgcn_s_setprio(FREI_PIPE_PRIO);
+#endif
   const int64_t nl = a.n_lam;
   const int64_t j0 = (int64_t)blockIdx.x * (64 * NC) + sub * 64 + lane;
   const bool act = j0 < nl;
@@ -2325,6 +2350,53 @@ __global__ __launch_bounds__(64 * NW) void sweep_chain_kernel(
   }
   sweep_group_body<DIR, Q, NW, true>(a, ss, Fu, Fd, part, dtaus, red, blockIdx.x - nU,
                                      gridDim.x - nU);
+}
+
+// The one-lane form chained (contracted single table, step records formed in the block).
+template <int DIR, int PD, int PF>
+__global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_chain_kernel(
+    FastArgs a, UpdateArgs u, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
+    double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
+  static_assert(kRedThreads == kBlock, "update workgroups of the sweep's block size");
+  extern __shared__ double red[];
+  const int nL = u.su.n_layers;
+  if ((int)blockIdx.x < nL) {
+    update_fused_body(u, blockIdx.x, nL, threadIdx.x, 0, red);
+    return;
+  }
+  sweep_fast_body<DIR, 1, PD, false, true, true, PF, true>(a, nullptr, ss, Fu, Fd, part, dtaus,
+                                                          red, blockIdx.x - nL, gridDim.x - nL);
+}
+
+template <int PD, int PF>
+static void launch_fast_chain_t(int dir, const FastArgs& a, const UpdateArgs& u, int nblocks,
+                                size_t shm, hipStream_t st) {
+  const int nL = u.su.n_layers;
+  const auto kernel = dir == kEmit ? sweep_fast_chain_kernel<kEmit, PD, PF>
+                                   : sweep_fast_chain_kernel<kAbsorb, PD, PF>;
+  hipLaunchKernelGGL(kernel, dim3(nL + nblocks), dim3(kBlock),
+                     sweep_shm(reinterpret_cast<const void*>(kernel), a, shm), st, a, u,
+                     a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+}
+
+// The one-lane sweep chained to the previous sweep's fused update u: depth 2 or 4 steps in
+// flight, loads pf (8, 16; 0: the depth) steps ahead, as launch_sweep_fast chooses them.
+void launch_sweep_fast_chain(int dir, int depth, int pf, const FastArgs& a, const UpdateArgs& u,
+                             int nblocks, hipStream_t st) {
+  size_t shm = (size_t)red_lds_doubles(a.red_rows, a.n_steps) * sizeof(double) +
+               (size_t)a.n_steps * sizeof(FastStepS) +
+               (size_t)rec_scratch_doubles(a) * sizeof(double);
+  const size_t ushm = (size_t)(2 * u.su.n_layers + u.su.n_tnodes) * sizeof(double);
+  if (ushm > shm) shm = ushm;
+  if (depth >= 4) {
+    if (pf >= 16) launch_fast_chain_t<4, 16>(dir, a, u, nblocks, shm, st);
+    else if (pf >= 8) launch_fast_chain_t<4, 8>(dir, a, u, nblocks, shm, st);
+    else launch_fast_chain_t<4, 4>(dir, a, u, nblocks, shm, st);
+  } else {
+    if (pf >= 16) launch_fast_chain_t<2, 16>(dir, a, u, nblocks, shm, st);
+    else if (pf >= 8) launch_fast_chain_t<2, 8>(dir, a, u, nblocks, shm, st);
+    else launch_fast_chain_t<2, 2>(dir, a, u, nblocks, shm, st);
+  }
 }
 
 // The chained launch of a grouped-lane sweep: the update workgroups of u ahead of nblocks sweep

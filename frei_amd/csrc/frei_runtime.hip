@@ -645,12 +645,13 @@ bool fused_ok(frei_ctx* c) {
          (2 * (size_t)c->nL + c->tnodes.size()) * sizeof(double) <= 32 * 1024;
 }
 
-// This sweep can run chained: the grouped-lane sweep forming its own records, fused update,
-// stream launches (no graph capture).
+// This sweep can run chained: a grouped-lane or one-lane (two or more steps in flight) sweep
+// of the contracted table forming its own step records, fused update, stream launches (no graph
+// capture).
 bool chain_ready(frei_ctx* c) {
   return c->chain && c->fast && c->eff && c->shared && records_in_sweep(c) &&
-         group_lanes(c) > 1 && pipe_consumers(c) == 0 && fused_ok(c) && !c->use_graph &&
-         !c->keys;
+         pipe_consumers(c) == 0 && fused_ok(c) && !c->use_graph && !c->keys &&
+         (group_lanes(c) > 1 || c->prefetch_depth != 1);
 }
 
 // Launch a deferred update on its own (the next sweep cannot take it, or the caller needs its
@@ -798,6 +799,12 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
       launch_sweep_chain(o.dir, Q, NW, f, u, nb_run, c->stream);
     } else if (Q > 1) {
       launch_sweep_group(o.dir, Q, NW, f, nb_run, c->stream);
+    } else if (merge) {   // the one-lane contracted sweep, records formed in the block
+      UpdateArgs u = c->pend;
+      u.epoch = c->d_epoch;
+      u.epoch_val = c->chain_seq;
+      c->has_pend = false;
+      launch_sweep_fast_chain(o.dir, depth, pf, f, u, c->nblocks, c->stream);
     } else {
       launch_sweep_fast(o.dir, S_run, depth, pf, nan_check && !c->eff, c->shared != 0, f,
                         c->nblocks, c->stream);

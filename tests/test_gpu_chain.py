@@ -4,7 +4,8 @@ temperatures it publishes (frei_kernels.hip sweep_chain_kernel, stage_records). 
 the sweep run the same code as in separate launches, so every output must be bit-identical:
 single sweeps, fixed-count iterations, runs to convergence (the converged flag then crosses a
 chained launch) — on the grouped-lane paths (two and four lanes per wavelength, 4- and 8-wave
-blocks, odd and even layer counts) and with the one-rank P2P exchange in the update."""
+blocks) and the one-lane path (two or four steps in flight), odd and even layer counts, and with
+the one-rank P2P exchange in the update."""
 import numpy as np
 import pytest
 
@@ -66,14 +67,18 @@ def _compare(a, b, tag):
 
 
 @pytest.mark.parametrize("nL", [30, 31])
-@pytest.mark.parametrize("q,waves", [(2, 4), (2, 8), (4, 4), (4, 8)])
-def test_chained_launches_are_bitwise_identical(fa, nL, q, waves):
+@pytest.mark.parametrize("q,waves,depth", [(2, 4, 0), (2, 8, 0), (4, 4, 0), (4, 8, 0),
+                                           (1, 4, 2), (1, 4, 4)])
+def test_chained_launches_are_bitwise_identical(fa, nL, q, waves, depth):
+    """Grouped-lane (Q = 2, 4) and one-lane (Q = 1; 2 or 4 steps in flight) sweeps."""
     lam, p, T0, tabs = _case(fa, nL)
     eng = fa.Engine(lam, p, tabs)
     out = {}
     try:
         eng.set_option("group_q", q)
         eng.set_option("group_waves", waves)
+        if depth:
+            eng.set_option("prefetch_depth", depth)
         for chain in (1, 0):
             eng.set_option("chain", chain)
             out[chain] = _exercise(eng, T0, nL, lam.size)
@@ -81,7 +86,7 @@ def test_chained_launches_are_bitwise_identical(fa, nL, q, waves):
     finally:
         eng.close()
     assert path["contracted"] and (path["paired"], path["quad"]) == (q == 2, q == 4)
-    _compare(out[1], out[0], f"Q{q} waves {waves} nL {nL}")
+    _compare(out[1], out[0], f"Q{q} waves {waves} depth {depth} nL {nL}")
     assert 1 < out[1]["run"]["n_iter"] <= 80
 
 
