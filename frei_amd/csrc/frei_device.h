@@ -389,6 +389,9 @@ void launch_sweep_group(int dir, int Q, int NW, const FastArgs& a, int nblocks, 
 // workgroups first, then the sweep blocks, which poll the new temperatures; single atmosphere).
 void launch_sweep_chain(int dir, int Q, int NW, const FastArgs& a, const UpdateArgs& u,
                         int nblocks, hipStream_t st);
+// The producer/consumer sweep (NC = 4) chained likewise.
+void launch_sweep_pipe_chain(int dir, int PF, const FastArgs& a, const UpdateArgs& u,
+                             int nblocks, hipStream_t st);
 // The one-lane contracted sweep (step records formed in the block) chained likewise.
 void launch_sweep_fast_chain(int dir, int depth, int pf, const FastArgs& a, const UpdateArgs& u,
                              int nblocks, hipStream_t st);

@@ -1347,11 +1347,12 @@ __host__ __device__ inline int64_t pipe_lds_doubles(int NC, int M, int ns) {
          (int64_t)NC * ns * 4 + (int64_t)ns * kStepDoubles;
 }
 
-template <int DIR, int NC, int M, int PF>
-__global__ __launch_bounds__(256 * NC) __attribute__((amdgpu_waves_per_eu(4)))
-void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
-                       double* __restrict__ Fd, double* __restrict__ part,
-                       double* __restrict__ dtaus) {
+template <int DIR, int NC, int M, int PF, bool CH>
+__device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __restrict__ ss,
+                                                double* __restrict__ Fu, double* __restrict__ Fd,
+                                                double* __restrict__ part,
+                                                double* __restrict__ dtaus, double* lds,
+                                                const int bx, const int nbx) {
   constexpr int G = kPipeP * M;   // steps per phase
   static_assert(PF == 1 || PF == 2, "table rows loaded one or two phases ahead");
   static_assert(G % 2 == 0, "phases hold whole step pairs (staged partial sums)");
@@ -1366,29 +1367,33 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
     a.ftoa += m * a.bs.ftoa;
     a.conv += m;
   }
-  if (!a.force && *a.conv) return;
+  if (!CH && !a.force && *a.conv) return;
   TRACE_DECL;
-  extern __shared__ double lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (a.poison && bx == 0)   // the deferred update's output temperatures: "not published"
+    for (int i = tid; i <= a.n_steps; i += 256 * NC)
+      reinterpret_cast<unsigned long long*>(a.poison)[i] = kPoisonT;
   const int sub = wv >> 2;    // 64-wavelength chunk of the block
   // 0 .. 2: producer, 3: consumer.  Waves w and w + 4 share a SIMD (profiles/r03/simd_map.txt),
-  // so role = w & 3 puts all four consumers on one SIMD and the producers' work on the other
-  // three; FREI_PIPE_ROT rotates the roles per chunk (every SIMD: three producers and one
-  // consumer), FREI_PIPE_PRIO raises the consumer's issue priority (its chain paces the phase).
+  // so role = w & 3 would put all four consumers on one SIMD and the producers' work on the
+  // other three.  The roles rotate per chunk (FREI_PIPE_ROT: every SIMD holds three producers
+  // and one consumer) and the consumer issues first (FREI_PIPE_PRIO: its chain paces the
+  // phase): together −4 µs per sweep at 62.5k λ (loop 33.2 → 29.6 µs,
+  // profiles/r03/pipe_layout/); either alone is no faster.
 #ifndef FREI_PIPE_ROT
-#define FREI_PIPE_ROT 0
+#define FREI_PIPE_ROT 1
 #endif
 #ifndef FREI_PIPE_PRIO
-#define FREI_PIPE_PRIO 0
+#define FREI_PIPE_PRIO 2
 #endif
   const int role = FREI_PIPE_ROT ? ((wv + sub) & 3) : (wv & 3);
 #if FREI_PIPE_PRIO
   if (role == kPipeP) __builtin_amdgcn_s_setprio(FREI_PIPE_PRIO);
 #endif
   const int64_t nl = a.n_lam;
-  const int64_t j0 = (int64_t)blockIdx.x * (64 * NC) + sub * 64 + lane;
+  const int64_t j0 = (int64_t)bx * (64 * NC) + sub * 64 + lane;
   const bool act = j0 < nl;
   const int64_t j = act ? j0 : nl - 1;
   const int ns = a.n_steps;
@@ -1401,7 +1406,7 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
   // which is not in use yet) or copied from the global step table
   FastStepS* lrec = reinterpret_cast<FastStepS*>(red + (int64_t)NC * ns * 4);
   if (a.rec_on) {
-    (void)stage_records(a, DIR, lrec, lds);
+    if (stage_records(a, DIR, lrec, lds)) return;
   } else {
     const double* g = reinterpret_cast<const double*>(ss);
     double* l = reinterpret_cast<double*>(lrec);
@@ -1582,9 +1587,18 @@ void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __r
   for (int idx = tid; idx < ns * 4; idx += 256 * NC) {
     double s = red[idx];
     for (int w = 1; w < NC; ++w) s += red[(int64_t)w * ns * 4 + idx];
-    part[(int64_t)idx * gridDim.x + blockIdx.x] = s;
+    part[(int64_t)idx * nbx + bx] = s;
   }
-  TRACE_PUT(20 + NC);
+  TRACE_PUT(CH ? 50 + NC : 20 + NC);
+}
+
+template <int DIR, int NC, int M, int PF>
+__global__ __launch_bounds__(256 * NC) __attribute__((amdgpu_waves_per_eu(4)))
+void sweep_pipe_kernel(FastArgs a, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
+                       double* __restrict__ Fd, double* __restrict__ part,
+                       double* __restrict__ dtaus) {
+  extern __shared__ double lds[];
+  sweep_pipe_body<DIR, NC, M, PF, false>(a, ss, Fu, Fd, part, dtaus, lds, blockIdx.x, gridDim.x);
 }
 
 template <int DIR, int NC, int M, int PF>
@@ -2130,8 +2144,8 @@ __device__ __forceinline__ void update_arrive(const UpdateArgs& a, int nU, int i
   __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Layer lr of nU update workgroups, run by kRedThreads threads (tid) — half h of a 512-thread
-// block in a chained 8-wave launch (each half its own LDS: sh, and the [h] arrays below).  A
+// Layer lr of nU update workgroups, run by kRedThreads threads (tid) — part h of a 512- or
+// 1024-thread block in a chained launch (each part its own LDS: sh, and the [h] arrays below).  A
 // half past the last layer (lr >= n_layers, odd layer counts) computes the last layer again
 // with every side effect suppressed, so both halves meet the same block barriers.
 // sh: dynamic LDS of (2 n_layers + n_tnodes) doubles.
@@ -2149,11 +2163,11 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
   double* sTn = sh;                 // [nL] new T of layers l, l + 1 (the setup's T view)
   double* sP = sTn + nL;            // [nL] p of layers l, l + 1 (the setup's p view)
   double* sNodes = sP + nL;         // [n_tnodes] sorted T nodes
-  __shared__ double wsum_[2][kRedWaves][8];
-  __shared__ double tot_[2][8];        // this rank's sums of steps k0 (0..3) and k1 (4..7)
-  __shared__ PMeta sPm_[2][kMaxFastS];  // layer l's metadata per species (setup)
-  __shared__ SpecMeta sSp_[2][kMaxFastS];
-  __shared__ double sMm_[2][kMaxFastS];
+  __shared__ double wsum_[4][kRedWaves][8];
+  __shared__ double tot_[4][8];        // this rank's sums of steps k0 (0..3) and k1 (4..7)
+  __shared__ PMeta sPm_[4][kMaxFastS];  // layer l's metadata per species (setup)
+  __shared__ SpecMeta sSp_[4][kMaxFastS];
+  __shared__ double sMm_[4][kMaxFastS];
   auto& wsum = wsum_[h];
   double* tot = tot_[h];
   PMeta* sPm = sPm_[h];
@@ -2350,6 +2364,54 @@ __global__ __launch_bounds__(64 * NW) void sweep_chain_kernel(
   }
   sweep_group_body<DIR, Q, NW, true>(a, ss, Fu, Fd, part, dtaus, red, blockIdx.x - nU,
                                      gridDim.x - nU);
+}
+
+// The producer/consumer form chained: 1024-thread blocks, so each update workgroup's four
+// 256-thread parts take a layer each.
+template <int DIR, int PF>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
+void sweep_pipe_chain_kernel(FastArgs a, UpdateArgs u, const FastStepS* __restrict__ ss,
+                             double* __restrict__ Fu, double* __restrict__ Fd,
+                             double* __restrict__ part, double* __restrict__ dtaus) {
+  static_assert(kRedThreads == 256, "update parts of 256 threads");
+  extern __shared__ double lds[];
+  const int nL = u.su.n_layers;
+  const int nU = (nL + 3) / 4;
+  if ((int)blockIdx.x < nU) {
+    const int h = threadIdx.x >> 8;
+    update_fused_body(u, blockIdx.x * 4 + h, nL, threadIdx.x & 255, h,
+                      lds + (int64_t)h * (2 * nL + u.su.n_tnodes));
+    return;
+  }
+  sweep_pipe_body<DIR, 4, 2, PF, true>(a, ss, Fu, Fd, part, dtaus, lds, blockIdx.x - nU,
+                                       gridDim.x - nU);
+}
+
+// The producer/consumer sweep (4 consumers per block) chained to the previous sweep's update u.
+void launch_sweep_pipe_chain(int dir, int PF, const FastArgs& a, const UpdateArgs& u,
+                             int nblocks, hipStream_t st) {
+  const int nL = u.su.n_layers;
+  size_t shm = pipe_lds_bytes(4, 2, a.n_steps);
+  const size_t ushm = (size_t)4 * (2 * nL + u.su.n_tnodes) * sizeof(double);
+  if (ushm > shm) shm = ushm;
+  auto go = [&](auto kernel) {
+    static std::unordered_map<const void*, size_t> optin;
+    size_t& have = optin[reinterpret_cast<const void*>(kernel)];
+    if (shm > have) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      have = shm;
+    }
+    hipLaunchKernelGGL(kernel, dim3((nL + 3) / 4 + nblocks), dim3(1024), shm, st, a, u,
+                       a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
+  };
+  if (PF == 2) {
+    if (dir == kEmit) go(sweep_pipe_chain_kernel<kEmit, 2>);
+    else go(sweep_pipe_chain_kernel<kAbsorb, 2>);
+  } else {
+    if (dir == kEmit) go(sweep_pipe_chain_kernel<kEmit, 1>);
+    else go(sweep_pipe_chain_kernel<kAbsorb, 1>);
+  }
 }
 
 // The one-lane form chained (contracted single table, step records formed in the block).

@@ -561,9 +561,10 @@ SetupArgs setup_args(frei_ctx* c);
 // table with shared brackets — and the mixing ratios are fixed (no T-dependent chemistry).
 bool records_in_sweep(frei_ctx* c) {
   if (!(c->rec_sweep && c->fast && c->eff && c->shared && !c->chem_on)) return false;
-  // auto: not for the producer/consumer sweep (neutral to slower) nor for batched contexts
-  // (every (block, atmosphere) would form the records: C5 -2 %, profiles/r02_ab_rec_sweep.txt)
-  return c->rec_sweep > 0 || (pipe_consumers(c) == 0 && c->n_atm == 1);
+  // auto: not for batched contexts (every (block, atmosphere) would form the records: C5 -2 %,
+  // profiles/r02_ab_rec_sweep.txt), nor for the producer/consumer sweep unless its launches
+  // are chained (neutral to slower on their own; a chained sweep must form its records)
+  return c->rec_sweep > 0 || (c->n_atm == 1 && (pipe_consumers(c) == 0 || c->chain));
 }
 
 SetupArgs setup_args(frei_ctx* c) {
@@ -649,9 +650,15 @@ bool fused_ok(frei_ctx* c) {
 // of the contracted table forming its own step records, fused update, stream launches (no graph
 // capture).
 bool chain_ready(frei_ctx* c) {
-  return c->chain && c->fast && c->eff && c->shared && records_in_sweep(c) &&
-         pipe_consumers(c) == 0 && fused_ok(c) && !c->use_graph && !c->keys &&
-         (group_lanes(c) > 1 || c->prefetch_depth != 1);
+  if (!(c->chain && c->fast && c->eff && c->shared && records_in_sweep(c) && fused_ok(c) &&
+        !c->use_graph && !c->keys))
+    return false;
+  const int nc = pipe_consumers(c);
+  if (nc > 0) return nc == 4;              // producer/consumer, four consumers per block
+  if (group_lanes(c) > 1) return true;      // grouped-lane
+  // one-lane (two or more steps in flight): measured neutral to slower at 125k-500k
+  // (profiles/r03/chain/ab_onelane.txt), so only on request (FREI_CHAIN=2)
+  return c->chain == 2 && c->prefetch_depth != 1;
 }
 
 // Launch a deferred update on its own (the next sweep cannot take it, or the caller needs its
@@ -789,6 +796,12 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
       c->keys->push_back(arg_hash(h, cfg));
     }
     if (c->dry) {
+    } else if (NC > 0 && merge) {
+      UpdateArgs u = c->pend;
+      u.epoch = c->d_epoch;
+      u.epoch_val = c->chain_seq;
+      c->has_pend = false;
+      launch_sweep_pipe_chain(o.dir, c->pipe_pf, f, u, nb_run, c->stream);
     } else if (NC > 0) {
       launch_sweep_pipe(o.dir, NC, c->pipe_pf, f, nb_run, c->stream);
     } else if (Q > 1 && merge) {
@@ -1009,7 +1022,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "pipe_pf") c->pipe_pf = v == 1 ? 1 : 2;
   else if (k == "k7_mfma") c->k7_mfma = v != 0;
   else if (k == "group_waves") c->group_waves = v == 8 ? 8 : 4;
-  else if (k == "chain") c->chain = v != 0;
+  else if (k == "chain") c->chain = v < 0 ? 0 : (v > 2 ? 2 : v);
   else if (k == "sweep_lds_kb") c->sweep_lds_kb = v < 0 ? 0 : (v > 160 ? 160 : v);
   else if (k == "prefetch_steps") c->prefetch_steps = v >= 16 ? 16 : v >= 8 ? 8 : 0;
   else return fail("unknown option '" + k + "'");

@@ -68,26 +68,31 @@ def _compare(a, b, tag):
 
 @pytest.mark.parametrize("nL", [30, 31])
 @pytest.mark.parametrize("q,waves,depth", [(2, 4, 0), (2, 8, 0), (4, 4, 0), (4, 8, 0),
-                                           (1, 4, 2), (1, 4, 4)])
+                                           (1, 4, 2), (1, 4, 4), (1, 4, "pipe")])
 def test_chained_launches_are_bitwise_identical(fa, nL, q, waves, depth):
-    """Grouped-lane (Q = 2, 4) and one-lane (Q = 1; 2 or 4 steps in flight) sweeps."""
+    """Grouped-lane (Q = 2, 4), one-lane (Q = 1; 2 or 4 steps in flight; chained on request,
+    FREI_CHAIN=2) and producer/consumer (4 consumers per block) sweeps."""
     lam, p, T0, tabs = _case(fa, nL)
     eng = fa.Engine(lam, p, tabs)
     out = {}
     try:
         eng.set_option("group_q", q)
         eng.set_option("group_waves", waves)
-        if depth:
+        if depth == "pipe":
+            eng.set_option("pipe", 4)
+        elif depth:
             eng.set_option("prefetch_depth", depth)
-        for chain in (1, 0):
+        for chain in (2 if q == 1 and depth != "pipe" else 1, 0):
             eng.set_option("chain", chain)
             out[chain] = _exercise(eng, T0, nL, lam.size)
         path = eng.path()
     finally:
         eng.close()
     assert path["contracted"] and (path["paired"], path["quad"]) == (q == 2, q == 4)
-    _compare(out[1], out[0], f"Q{q} waves {waves} depth {depth} nL {nL}")
-    assert 1 < out[1]["run"]["n_iter"] <= 80
+    assert (path["pipe"] == 4) == (depth == "pipe")
+    on = max(out)
+    _compare(out[on], out[0], f"Q{q} waves {waves} depth {depth} nL {nL}")
+    assert 1 < out[on]["run"]["n_iter"] <= 80
 
 
 def test_chained_launches_with_p2p_exchange(fa):
