@@ -199,11 +199,11 @@ struct frei_ctx {
   int pair_max_blocks = 420;            // FREI_PAIR_MAX_BLOCKS (<= 107k lambda per GPU)
   int quad_max_blocks = 208;            // FREI_QUAD_MAX_BLOCKS (<= 53k lambda per GPU)
   int group_q = 0;                      // FREI_GROUP_Q forces 1, 2 or 4 lanes per wavelength
-  int pipe_nc = 0;                      // FREI_PIPE: producer/consumer sweep, 1/2/4 consumers per
-                                        // block, 0 off (default since round 3: two lanes per
-                                        // wavelength with in-sweep records give the shorter
-                                        // T-P iteration at 62.5k, profiles/r03/slice_forms.txt),
-                                        // -1 by slice size (pipe_*_blocks)
+  int pipe_nc = -1;                     // FREI_PIPE: producer/consumer sweep, 1/2/4 consumers per
+                                        // block, 0 off, -1 by slice size (pipe_*_blocks; the
+                                        // default again since its roles were balanced over the
+                                        // SIMDs: -2 % per T-P iteration at 62.5k with P2P vs
+                                        // the chained grouped-lane form, profiles/r03/chain/)
   int pipe_min_blocks = 208;            // FREI_PIPE_MIN_BLOCKS / _MAX_BLOCKS: 256-wavelength
   int pipe_max_blocks = -1;             // blocks per GPU where the auto choice takes NC = 4
                                         // (-1: the CU count, one 16-wave block per CU)
@@ -564,7 +564,7 @@ bool records_in_sweep(frei_ctx* c) {
   // auto: not for batched contexts (every (block, atmosphere) would form the records: C5 -2 %,
   // profiles/r02_ab_rec_sweep.txt), nor for the producer/consumer sweep unless its launches
   // are chained (neutral to slower on their own; a chained sweep must form its records)
-  return c->rec_sweep > 0 || (c->n_atm == 1 && (pipe_consumers(c) == 0 || c->chain));
+  return c->rec_sweep > 0 || (c->n_atm == 1 && (pipe_consumers(c) == 0 || c->chain == 2));
 }
 
 SetupArgs setup_args(frei_ctx* c) {
@@ -654,7 +654,13 @@ bool chain_ready(frei_ctx* c) {
         !c->use_graph && !c->keys))
     return false;
   const int nc = pipe_consumers(c);
-  if (nc > 0) return nc == 4;              // producer/consumer, four consumers per block
+  // producer/consumer, four consumers per block; the chained kernel adds the update body's
+  // static LDS (4.3 KiB) to the sweep's, which must still fit the CU (deep atmospheres do not)
+  // — only on request (FREI_CHAIN=2): chained, its 1024-thread update blocks take 6 µs where
+  // the separate update kernel takes 3 (profiles/r03/chain/ab_pipe.txt)
+  if (nc > 0)
+    return c->chain == 2 && nc == 4 &&
+           pipe_lds_bytes(4, c->pipe_m, c->nL - 1) + 6 * 1024 <= c->lds_optin;
   if (group_lanes(c) > 1) return true;      // grouped-lane
   // one-lane (two or more steps in flight): measured neutral to slower at 125k-500k
   // (profiles/r03/chain/ab_onelane.txt), so only on request (FREI_CHAIN=2)

@@ -70,8 +70,8 @@ def _compare(a, b, tag):
 @pytest.mark.parametrize("q,waves,depth", [(2, 4, 0), (2, 8, 0), (4, 4, 0), (4, 8, 0),
                                            (1, 4, 2), (1, 4, 4), (1, 4, "pipe")])
 def test_chained_launches_are_bitwise_identical(fa, nL, q, waves, depth):
-    """Grouped-lane (Q = 2, 4), one-lane (Q = 1; 2 or 4 steps in flight; chained on request,
-    FREI_CHAIN=2) and producer/consumer (4 consumers per block) sweeps."""
+    """Grouped-lane (Q = 2, 4), one-lane (Q = 1; 2 or 4 steps in flight) and producer/consumer
+    (4 consumers per block) sweeps; the latter two are chained only on request (FREI_CHAIN=2)."""
     lam, p, T0, tabs = _case(fa, nL)
     eng = fa.Engine(lam, p, tabs)
     out = {}
@@ -82,7 +82,7 @@ def test_chained_launches_are_bitwise_identical(fa, nL, q, waves, depth):
             eng.set_option("pipe", 4)
         elif depth:
             eng.set_option("prefetch_depth", depth)
-        for chain in (2 if q == 1 and depth != "pipe" else 1, 0):
+        for chain in (2 if q == 1 else 1, 0):   # one-lane and pipe: chained on request
             eng.set_option("chain", chain)
             out[chain] = _exercise(eng, T0, nL, lam.size)
         path = eng.path()

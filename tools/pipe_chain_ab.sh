@@ -5,11 +5,10 @@
 set -e -o pipefail
 O=gpurun_out/${1:-pchain}
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_chain.py tests/test_gpu_parity.py -k "chain or pipe" -x -q --timeout 200 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }
-tail -1 $O/pytest.txt
+[ -n "$SKIP_TESTS" ] || { timeout -k 10 300 python -u -m pytest tests/test_gpu_chain.py tests/test_gpu_parity.py -k "chain or pipe" -x -q --timeout 200 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -30 $O/pytest.txt; exit 1; }; tail -1 $O/pytest.txt; }
 T="timeout -k 10 120 python3 tools/trace_probe.py --n-lam 62500"
-FREI_HIP_LIB=abv/trace.so FREI_PIPE=4 $T 2>/dev/null > $O/t_pipe_chain.txt; echo "== pipe chain"; grep -A4 "update_fused'," $O/t_pipe_chain.txt
-FREI_HIP_LIB=abv/trace.so FREI_PIPE=4 FREI_CHAIN=0 $T 2>/dev/null > $O/t_pipe.txt; echo "== pipe"; grep -A3 "kind" $O/t_pipe.txt; grep half $O/t_pipe.txt
+FREI_HIP_LIB=abv/trace.so FREI_PIPE=4 $T 2>/dev/null > $O/t_pipe_chain.txt; echo "== pipe chain"; cat $O/t_pipe_chain.txt
+FREI_HIP_LIB=abv/trace.so FREI_PIPE=4 FREI_CHAIN=0 $T 2>/dev/null > $O/t_pipe.txt; echo "== pipe"; cat $O/t_pipe.txt
 B="python3 bench.py --n-lam 62500 --steps 40 --warmup 5 --rad-eq-max 1 --no-binning --no-cpu-baseline --no-c5 --no-per-species --no-chemistry"
 for r in 1 2 3; do
   for cfg in "0 1" "4 0" "4 1"; do
