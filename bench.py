@@ -51,6 +51,12 @@ def parse():
                     help="N > 1 exchange: the engine's P2P mailboxes over xGMI (default; falls "
                          "back to RCCL if they cannot be set up), RCCL all-gather, or the host "
                          "hook (lets several ranks share one GPU to rehearse the multi-rank flow)")
+    ap.add_argument("--lam-slice", default=None,
+                    help="LO:HI — one GPU runs only this slice of the --n-lam grid (global "
+                         "trapezoid weights), as one rank of a multi-GPU run would: projection")
+    ap.add_argument("--balance", action="store_true",
+                    help="re-split the wavelength grid across GPUs to equal measured per-rank sweep "
+                         "time before timing (default: the even split)")
     ap.add_argument("--force-comm", action="store_true",
                     help="with --gpus 1: still join the exchange (a one-rank P2P mailbox or "
                          "RCCL communicator), to time its per-sweep cost on one GPU")
@@ -94,6 +100,12 @@ class Dist:
         if not self.rdzv:
             return bool(ok)
         return all(v == b"1" for v in self.rdzv.all_gather(b"1" if ok else b"0"))
+
+    def gather(self, x):
+        """Every rank's float x, in rank order."""
+        if not self.rdzv:
+            return [float(x)]
+        return [float(v) for v in self.rdzv.all_gather(repr(float(x)).encode())]
 
 
 def cpu_baseline(w, n_sample, steps=1):
@@ -387,43 +399,78 @@ def main():
     w = c3(n_layers=a.n_layers, n_lam=a.n_lam, n_T=a.n_T)
     nL, n_lam, S = a.n_layers, a.n_lam, len(w["names"])
     lo, hi = partition(n_lam, d.world, d.rank)
+    if a.lam_slice:
+        if d.world != 1:
+            raise SystemExit("--lam-slice is a one-GPU projection option")
+        lo, hi = (int(x) for x in a.lam_slice.split(":"))
     tabs = {n: SeparableTable(w["base"][s], w["fp"][s], w["fT"][s], w["p"], w["T_nodes"])
             for s, n in enumerate(w["names"])}
-    kind, comm_note = a.comm, None
-    t_e = time.perf_counter()
-    eng, err = None, None
-    try:
-        eng = build_engine(w, tabs, lo, hi, d, kind, a.force_comm)
-    except RuntimeError as e:   # e.g. no IPC / peer mapping: fall back to RCCL everywhere
-        err = str(e)
-    if not d.all_ok(eng is not None):
-        if kind != "p2p":
-            raise SystemExit(f"rank {d.rank}: engine setup failed: {err}")
-        if eng is not None:
-            eng.close()
-        eng, kind, comm_note = build_engine_fallback(
-            w, tabs, lo, hi, d, a.force_comm, f"p2p setup failed ({err or 'on a peer rank'})")
-    tables_s = time.perf_counter() - t_e
-    # one-time setup: metadata build + species contraction (K3), outside the timed steps
-    t_s = time.perf_counter()
-    path = eng.path()
-    setup_ms = (time.perf_counter() - t_s) * 1e3
-    setup_phases = eng.setup_timing()
-    if kind == "p2p" and d.world > 1:
-        # one untimed T-P iteration through the mailboxes: a peer whose sums never arrive
-        # fails every rank within FREI_P2P_TIMEOUT_S, and the run goes on over RCCL instead
-        err = None
+
+    def make_engine(lo, hi, kind):
+        """This rank's engine for [lo, hi) over `kind`, with the fallback chain P2P -> RCCL ->
+        host; then its one-time setup (metadata + K3) and, over P2P, one untimed iteration
+        through the mailboxes.  Returns (engine, kind, note, tables_s, path, setup_ms, phases)."""
+        comm_note = None
+        t_e = time.perf_counter()
+        eng, err = None, None
         try:
-            eng.state_init(w["T0"])
-            eng.iterate(1)
-            eng.synchronize()
-        except RuntimeError as e:
+            eng = build_engine(w, tabs, lo, hi, d, kind, a.force_comm)
+        except RuntimeError as e:   # e.g. no IPC / peer mapping: fall back to RCCL everywhere
             err = str(e)
-        if not d.all_ok(err is None):
-            eng.close()
+        if not d.all_ok(eng is not None):
+            if kind != "p2p":
+                raise SystemExit(f"rank {d.rank}: engine setup failed: {err}")
+            if eng is not None:
+                eng.close()
             eng, kind, comm_note = build_engine_fallback(
-                w, tabs, lo, hi, d, a.force_comm,
-                f"p2p exchange failed at run time ({err or 'on a peer rank'})")
+                w, tabs, lo, hi, d, a.force_comm, f"p2p setup failed ({err or 'on a peer rank'})")
+        tables_s = time.perf_counter() - t_e
+        # one-time setup: metadata build + species contraction (K3), outside the timed steps
+        t_s = time.perf_counter()
+        path = eng.path()
+        setup_ms = (time.perf_counter() - t_s) * 1e3
+        setup_phases = eng.setup_timing()
+        if kind == "p2p" and d.world > 1:
+            # one untimed T-P iteration through the mailboxes: a peer whose sums never arrive
+            # fails every rank within FREI_P2P_TIMEOUT_S, and the run goes on over RCCL instead
+            err = None
+            try:
+                eng.state_init(w["T0"])
+                eng.iterate(1)
+                eng.synchronize()
+            except RuntimeError as e:
+                err = str(e)
+            if not d.all_ok(err is None):
+                eng.close()
+                eng, kind, comm_note = build_engine_fallback(
+                    w, tabs, lo, hi, d, a.force_comm,
+                    f"p2p exchange failed at run time ({err or 'on a peer rank'})")
+        return eng, kind, comm_note, tables_s, path, setup_ms, setup_phases
+
+    eng, kind, comm_note, tables_s, path, setup_ms, setup_phases = make_engine(lo, hi, a.comm)
+    # ---- cost-balanced slices (--balance): every rank times its sweeps on the even split and the
+    # grid is re-split to equal measured cost (frei_amd.balanced_edges) before anything is
+    # timed.  Off by default: at the 8-GPU slice the producer/consumer sweep's time is one
+    # block's loop (one 256-wavelength block per CU), which a smaller slice does not shorten, and
+    # at the 4-GPU slice a larger slice can cross a sweep-form threshold (profiles/r03/projection/
+    # balanced.txt: 165 -> 191 us); the slower long-wavelength ranks (DESIGN.md §6) stay.
+    slicing = {"kind": "even", "edges": [partition(n_lam, d.world, r)[0]
+                                         for r in range(d.world)] + [n_lam]}
+    if d.world > 1 and a.balance:
+        from frei_amd.engine import balanced_edges
+        eng.state_init(w["T0"])
+        eng.iterate(2)
+        eng.synchronize()
+        ms_even = d.gather(sweep_kernel_time(eng, 4)[0])
+        edges = balanced_edges(slicing["edges"], ms_even)
+        moved = edges != slicing["edges"]   # the same decision on every rank
+        slicing = {"kind": "cost-balanced (per-rank sweep time on the even split)",
+                   "edges": edges, "even_sweep_ms": ms_even}
+        if moved:
+            lo, hi = edges[d.rank], edges[d.rank + 1]
+            eng.close()
+            eng, kind, comm_note, tables_s, path, setup_ms, setup_phases = make_engine(
+                lo, hi, kind)
 
     # ---- headline: timed fixed-work T-P iterations (no per-kernel events inside)
     eng.state_init(w["T0"])
@@ -441,7 +488,7 @@ def main():
                                           if kind == "p2p" else
                                           "stream time of the all-gather, per sweep "
                                           "(includes waiting for the slowest rank)")}
-    updates_per_step = 2 * (nL - 1) * n_lam
+    updates_per_step = 2 * (nL - 1) * (hi - lo if a.lam_slice else n_lam)
     value = updates_per_step * a.steps / elapsed
     ms_per_step = elapsed / a.steps * 1e3
 
@@ -590,7 +637,8 @@ def main():
                        "n_layers": nL, "n_lambda": n_lam, "n_species": S, "n_T": a.n_T,
                        "parallelism": f"lambda-shard x{d.world}"
                                       + ("" if d.world == 1 and not a.force_comm
-                                         else f" ({kind} exchange per sweep)")},
+                                         else f" ({kind} exchange per sweep)"),
+                       "slicing": slicing},
             "tp_iters_per_s": 1e3 / ms_per_step,
             "exchange": exchange,
             "sweep_path": dict(path, setup_ms=setup_ms, setup_phases_ms=setup_phases,

@@ -11,7 +11,7 @@ from .chemistry import ChemistryTable, chemistry, iso_to_mass, iso_to_species
 from .core import (B_star, F_TOA, Grid, Planet, Spectrum, contribution_function,
                    effective_temperature,
                    effective_temperature_milne, effective_temperature_planck, wavelength_grid)
-from .engine import Engine, partition, trapz_weights
+from .engine import Engine, balanced_edges, partition, trapz_weights
 from .opacity import (OpacityTable, SeparableTable, binned_opacity, kappa,
                       load_example_opacity, rayleigh_H2, rayleigh_He)
 from .tp import pressure_grid, temperature_grid
@@ -23,6 +23,6 @@ __all__ = ["Planet", "Grid", "Spectrum", "effective_temperature", "wavelength_gr
            "B_star", "kappa", "load_example_opacity", "OpacityTable", "SeparableTable",
            "binned_opacity", "rayleigh_H2", "rayleigh_He", "chemistry", "iso_to_species",
            "iso_to_mass", "pressure_grid", "temperature_grid", "propagate_fluxes", "emit",
-           "absorb", "BB", "E", "Engine", "partition", "trapz_weights", "CrossSection",
+           "absorb", "BB", "E", "Engine", "balanced_edges", "partition", "trapz_weights", "CrossSection",
            "BinnedTable", "open_cross_section", "contribution_function", "BatchEngine",
            "batched_emission_spectra", "ChemistryTable"]

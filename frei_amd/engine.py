@@ -54,6 +54,32 @@ def partition(n, nranks, rank):
     return lo, lo + base + (1 if rank < rem else 0)
 
 
+def balanced_edges(edges, costs, align=256):
+    """Slice edges of equal measured cost.
+
+    ``edges`` = [0, e_1, ..., n]: the current contiguous slices, ``costs`` = each slice's
+    measured time (e.g. its sweep kernel's).  The cost per wavelength is taken as constant inside
+    each current slice, and the new edges split the cumulative cost into equal parts, rounded to
+    multiples of ``align`` wavelengths (whole sweep blocks) and kept strictly increasing.  The
+    per-wavelength work of the sweep depends on the data (the opacities, the temperatures), so
+    an even split leaves some ranks on the critical path of every exchange.
+    """
+    edges = np.asarray(edges, dtype=np.int64)
+    costs = np.asarray(costs, dtype=float)
+    R, n = len(costs), int(edges[-1])
+    if len(edges) != R + 1 or np.any(np.diff(edges) <= 0) or np.any(costs <= 0):
+        raise ValueError("edges must increase and bound len(costs) slices of positive cost")
+    cum = np.concatenate([[0.0], np.cumsum(costs)])          # cumulative cost at the edges
+    out = [0]
+    for k in range(1, R):
+        x = float(np.interp(cum[-1] * k / R, cum, edges))   # piecewise-linear inverse
+        e = int(round(x / align)) * align
+        e = min(max(e, out[-1] + align), n - (R - k) * align)
+        out.append(e)
+    out.append(n)
+    return out
+
+
 def _table_arrays(tab):
     p = np.asarray(value(tab.pressure, "bar"), dtype=float)
     T = np.asarray(value(tab.temperature, "K"), dtype=float)

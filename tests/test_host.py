@@ -118,3 +118,24 @@ def test_chemistry_table_interpolation_contract():
     assert np.array_equal(c(9e3, 1e5), vals[:, -1, -1])     # clamped above
     t = fa.ChemistryTable({"12C-16O": vals[1], "1H2-16O": vals[0]}, T, p)
     assert np.array_equal(t.array(["1H2-16O", "12C-16O"]), vals)
+
+
+def test_balanced_edges_split_the_measured_cost_evenly():
+    """Cost-balanced wavelength slices (bench.py's multi-GPU calibration): equal costs keep an
+    even split, a slice twice as expensive per wavelength is shrunk, edges stay block-aligned."""
+    from frei_amd.engine import balanced_edges, partition
+    n, R = 500_000, 8
+    even = [partition(n, R, r)[0] for r in range(R)] + [n]
+    e = balanced_edges(even, [1.0] * R)
+    assert e[0] == 0 and e[-1] == n and all(b > a for a, b in zip(e, e[1:]))
+    assert max(abs(a - b) for a, b in zip(e, even)) <= 256
+    assert all(x % 256 == 0 for x in e[:-1])
+    # the last slice costs twice as much per wavelength: the new split equalises the cost
+    costs = [1.0] * (R - 1) + [2.0]
+    e = balanced_edges(even, costs)
+    dens = np.repeat(np.array(costs) / np.diff(even), np.diff(even))
+    per = [dens[a:b].sum() for a, b in zip(e, e[1:])]
+    assert max(per) / min(per) < 1.01
+    assert e[-1] - e[-2] < n // R
+    with pytest.raises(ValueError):
+        balanced_edges([0, 10, 5], [1.0, 1.0])
