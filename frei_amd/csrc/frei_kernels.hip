@@ -2338,6 +2338,21 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
   TRACE_PUT(30);
 }
 
+// The barriers of update_fused_body for the threads of a chained launch's update block that
+// update no layer (the producer/consumer form's 1024-thread blocks: threads 0..255 update one
+// layer, the other 768 only meet the body's block barriers).  The body has three barriers, none
+// on its converged path; *a.conv is read before the first, and it is only written by the last
+// layer to arrive, after every block has passed its second barrier — so both reads agree.
+__device__ __forceinline__ void update_shadow(const UpdateArgs& a) {
+#ifdef FREI_UPD_EMPTY
+  return;
+#endif
+  if (!a.force && *a.conv) return;
+  __syncthreads();
+  __syncthreads();
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sh[];
   update_fused_body(a, blockIdx.x, gridDim.x, threadIdx.x, 0, sh);
@@ -2366,8 +2381,9 @@ __global__ __launch_bounds__(64 * NW) void sweep_chain_kernel(
                                      gridDim.x - nU);
 }
 
-// The producer/consumer form chained: 1024-thread blocks, so each update workgroup's four
-// 256-thread parts take a layer each.
+// The producer/consumer form chained: 1024-thread blocks, one layer per update block (its first
+// 256 threads; the other 768 only meet the update's barriers, update_shadow) — four layers per
+// block measured slower: the partial-sum loads of four layers queue on one CU.
 template <int DIR, int PF>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
 void sweep_pipe_chain_kernel(FastArgs a, UpdateArgs u, const FastStepS* __restrict__ ss,
@@ -2376,15 +2392,13 @@ void sweep_pipe_chain_kernel(FastArgs a, UpdateArgs u, const FastStepS* __restri
   static_assert(kRedThreads == 256, "update parts of 256 threads");
   extern __shared__ double lds[];
   const int nL = u.su.n_layers;
-  const int nU = (nL + 3) / 4;
-  if ((int)blockIdx.x < nU) {
-    const int h = threadIdx.x >> 8;
-    update_fused_body(u, blockIdx.x * 4 + h, nL, threadIdx.x & 255, h,
-                      lds + (int64_t)h * (2 * nL + u.su.n_tnodes));
+  if ((int)blockIdx.x < nL) {
+    if (threadIdx.x < 256) update_fused_body(u, blockIdx.x, nL, threadIdx.x, 0, lds);
+    else update_shadow(u);
     return;
   }
-  sweep_pipe_body<DIR, 4, 2, PF, true>(a, ss, Fu, Fd, part, dtaus, lds, blockIdx.x - nU,
-                                       gridDim.x - nU);
+  sweep_pipe_body<DIR, 4, 2, PF, true>(a, ss, Fu, Fd, part, dtaus, lds, blockIdx.x - nL,
+                                       gridDim.x - nL);
 }
 
 // The producer/consumer sweep (4 consumers per block) chained to the previous sweep's update u.
@@ -2392,7 +2406,7 @@ void launch_sweep_pipe_chain(int dir, int PF, const FastArgs& a, const UpdateArg
                              int nblocks, hipStream_t st) {
   const int nL = u.su.n_layers;
   size_t shm = pipe_lds_bytes(4, 2, a.n_steps);
-  const size_t ushm = (size_t)4 * (2 * nL + u.su.n_tnodes) * sizeof(double);
+  const size_t ushm = (size_t)(2 * nL + u.su.n_tnodes) * sizeof(double);
   if (ushm > shm) shm = ushm;
   auto go = [&](auto kernel) {
     static std::unordered_map<const void*, size_t> optin;
@@ -2402,7 +2416,7 @@ void launch_sweep_pipe_chain(int dir, int PF, const FastArgs& a, const UpdateArg
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
       have = shm;
     }
-    hipLaunchKernelGGL(kernel, dim3((nL + 3) / 4 + nblocks), dim3(1024), shm, st, a, u,
+    hipLaunchKernelGGL(kernel, dim3(nL + nblocks), dim3(1024), shm, st, a, u,
                        a.ssteps, a.F_up, a.F_down, a.part, a.dtaus);
   };
   if (PF == 2) {
