@@ -234,12 +234,22 @@ __device__ __forceinline__ double exp_neg_nf(double x) {
 // 1 / b within one ulp: the reciprocal part of the division core below (rcp and two
 // Newton-Raphson steps) without the quotient's final residual correction.  Used where the
 // result only scales a sum (1 / chi of the flux update), so an ulp is not amplified.
+// FREI_RCP_STEPS: Newton steps after v_rcp_f64 — 2 (default): within 1 ulp; 1: within 11 ulp,
+// two VALU fewer per update, 0..1.5 % sweep time (noise-level, profiles/r03/ab_rcp_steps.txt) but
+// batched-vs-single temperatures then differ by 2e-11 after 3 iterations: not adopted.
+#ifndef FREI_RCP_STEPS
+#define FREI_RCP_STEPS 2
+#endif
 __device__ __forceinline__ double rcp_nr(double b) {
   double r = __builtin_amdgcn_rcp(b);
   double e = __builtin_fma(-b, r, 1.0);
+#if FREI_RCP_STEPS == 1
+  return __builtin_fma(r, e, r);
+#else
   r = __builtin_fma(r, e, r);
   e = __builtin_fma(-b, r, 1.0);
   return __builtin_fma(r, e, r);
+#endif
 }
 
 // a / b: LLVM's fp64 division core (rcp, two Newton-Raphson steps — one with FREI_FM_DIV 2 —,
