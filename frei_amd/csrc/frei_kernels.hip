@@ -1385,6 +1385,9 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
 #ifndef FREI_PIPE_ROT
 #define FREI_PIPE_ROT 1
 #endif
+#ifndef FREI_PIPE_SPF   // phases ahead the consumer loads its stale fluxes (1 or 2)
+#define FREI_PIPE_SPF 1
+#endif
 #ifndef FREI_PIPE_PRIO
 #define FREI_PIPE_PRIO 2
 #endif
@@ -1474,6 +1477,15 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
       bool e1 = true;
 #pragma unroll
       for (int i = 0; i < M; ++i) e1 = e1 && !(pc[i].w0 > 0.1);
+#ifdef FREI_PIPE_NOPROD   // diagnostic ablation build: trivial coefficients, same loads / stores
+      if (true) {
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          c[i].psi = pc[i].w0; c[i].xi = pc[i].dtau; c[i].ic = 0.5; c[i].Xu = pc[i].B1;
+          c[i].Xd = pc[i].B2; c[i].dtau = pc[i].dtau;
+        }
+      } else
+#endif
       if (__all(e1)) {
 #pragma unroll
         for (int i = 0; i < M; ++i)   // contracted table: NaN-free
@@ -1517,70 +1529,112 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
     const double wt = act ? a.wtr[j] : 0.0;
     double carry = (DIR == kEmit) ? Fu[(int64_t)step_layer(DIR, 0, nL) * nl + j]
                                   : Fd[(int64_t)(step_layer(DIR, 0, nL) + 1) * nl + j];
-    double stn[G];   // stale opposite-stream fluxes of the next phase
-    auto load_stale = [&](int ph) {
-#pragma unroll
-      for (int i = 0; i < G; ++i) {
-        const int k = min(ph * G + i, ns - 1);
+    // the stale opposite-stream flux of step ph G + i (clamped past the last step)
+    auto stale = [&](int ph, int i) {
+      const int k = min(ph * G + i, ns - 1);
+      const int layer = step_layer(DIR, k, nL);
+      const double* src = (DIR == kEmit)
+                              ? (k == ns - 1 ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
+                              : Fu + (int64_t)layer * nl;
+#ifdef FREI_PIPE_STALE_HOT   // diagnostic ablation build: stale loads from one cached row
+      return a.ftoa[j] + 0.0 * src[0];
+#else
+      return src[j];
+#endif
+    };
+    double* t0 = tile + (int64_t)sub * 2 * 4 * kStageRow;
+    // step i of phase q: the carried chain, flux stores and staged bolometric terms (a pair's
+    // 8 sums after its second step)
+    auto step = [&](int q, int i, double stv) {
+      const int k = q * G + i;
+      if (k < ns) {
+        const double psi = *rslot(q, i, 0), xi = *rslot(q, i, 1), ic = *rslot(q, i, 2);
+        const double Xu = *rslot(q, i, 3), Xd = *rslot(q, i, 4);
+        double F1u, F2d;
+        if (DIR == kEmit) { F1u = carry; F2d = stv; } else { F2d = carry; F1u = stv; }
+        const double F2u = ic * ((psi * F1u - xi * F2d) + Xu);
+        const double F1d = ic * ((psi * F2d - xi * F1u) + Xd);
         const int layer = step_layer(DIR, k, nL);
-        const double* src = (DIR == kEmit)
-                                ? (k == ns - 1 ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
-                                : Fu + (int64_t)layer * nl;
-        stn[i] = src[j];
+        const bool top = DIR == kEmit && k == ns - 1;
+#ifndef FREI_PIPE_NOSTORE   // diagnostic ablation build: no flux stores
+        if (act) {
+          const bool st_up = (DIR == kEmit) ? !top : (!a.live_only || layer == 0);
+          const bool st_dn = (DIR == kAbsorb) || !a.live_only || top;
+          if (st_up) flux_store(Fu + (int64_t)(layer + 1) * nl + j, F2u);
+          if (st_dn) flux_store(Fd + (int64_t)layer * nl + j, F1d);
+        }
+#endif
+        double* t = t0 + ((k & 1) * 4) * kStageRow + lane;
+        t[0] = wt * F2u;
+        t[kStageRow] = wt * F2d;
+        t[2 * kStageRow] = wt * F1u;
+        t[3 * kStageRow] = wt * F1d;
+        carry = (DIR == kEmit) ? F2u : F1d;
+      }
+#ifdef FREI_PIPE_NORED   // diagnostic ablation build: no bolometric reduction
+      if (false) {
+#else
+      if (i & 1) {   // the pair's 8 (step, quantity) sums: the one-lane staged reduction
+#endif
+        __builtin_amdgcn_wave_barrier();
+        const int o = lane >> 3;
+        const double* t = t0 + ((o >> 2) * 4 + (o & 3)) * kStageRow + (lane & 7);
+        double y = t[0];
+#pragma unroll
+        for (int r = 1; r < 8; ++r) y += t[8 * r];
+        y += dpp_bcast<0xB1>(y);    // quad_perm [1,0,3,2]
+        y += dpp_bcast<0x4E>(y);    // quad_perm [2,3,0,1]
+        y += dpp_bcast<0x141>(y);   // row_half_mirror
+        const int ks = k - 1 + (o >> 2);
+        if ((lane & 7) == 0 && ks < ns) red[((int64_t)sub * ns + ks) * 4 + (o & 3)] = y;
+        __builtin_amdgcn_wave_barrier();
       }
     };
-    load_stale(0);
-    double* t0 = tile + (int64_t)sub * 2 * 4 * kStageRow;
+#if FREI_PIPE_SPF == 2
+    // stale fluxes loaded two phases ahead: two register buffers (phases alternate, the loop
+    // is unrolled by two), each element refilled right after its step has used it
+    double sA[G], sB[G];
+#pragma unroll
+    for (int i = 0; i < G; ++i) sA[i] = stale(0, i);
+#pragma unroll
+    for (int i = 0; i < G; ++i) sB[i] = stale(1, i);
+    auto consume = [&](int q, double (&sv)[G]) {
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        step(q, i, sv[i]);
+        sv[i] = stale(q + 2, i);
+      }
+    };
+    for (int ph = 0; ph <= nph; ph += 2) {   // nph + 1 barriers, like the producers'
+      if (ph >= 1) consume(ph - 1, sB);
+      __syncthreads();
+      if (ph + 1 <= nph) {
+        consume(ph, sA);
+        __syncthreads();
+      }
+    }
+#else
+    double stn[G];   // stale opposite-stream fluxes of the next phase
+#pragma unroll
+    for (int i = 0; i < G; ++i) stn[i] = stale(0, i);
     for (int ph = 0; ph <= nph; ++ph) {
+#ifdef FREI_PIPE_NOCONS   // diagnostic ablation build: the consumer only meets the barriers
+      if (false) {
+#else
       if (ph >= 1) {
+#endif
         const int q = ph - 1;   // phase consumed now
         double stc[G];
 #pragma unroll
         for (int i = 0; i < G; ++i) stc[i] = stn[i];
-        load_stale(ph);
 #pragma unroll
-        for (int i = 0; i < G; ++i) {
-          const int k = q * G + i;
-          if (k < ns) {
-            const double psi = *rslot(q, i, 0), xi = *rslot(q, i, 1), ic = *rslot(q, i, 2);
-            const double Xu = *rslot(q, i, 3), Xd = *rslot(q, i, 4);
-            double F1u, F2d;
-            if (DIR == kEmit) { F1u = carry; F2d = stc[i]; } else { F2d = carry; F1u = stc[i]; }
-            const double F2u = ic * ((psi * F1u - xi * F2d) + Xu);
-            const double F1d = ic * ((psi * F2d - xi * F1u) + Xd);
-            const int layer = step_layer(DIR, k, nL);
-            const bool top = DIR == kEmit && k == ns - 1;
-            if (act) {
-              const bool st_up = (DIR == kEmit) ? !top : (!a.live_only || layer == 0);
-              const bool st_dn = (DIR == kAbsorb) || !a.live_only || top;
-              if (st_up) flux_store(Fu + (int64_t)(layer + 1) * nl + j, F2u);
-              if (st_dn) flux_store(Fd + (int64_t)layer * nl + j, F1d);
-            }
-            double* t = t0 + ((k & 1) * 4) * kStageRow + lane;
-            t[0] = wt * F2u;
-            t[kStageRow] = wt * F2d;
-            t[2 * kStageRow] = wt * F1u;
-            t[3 * kStageRow] = wt * F1d;
-            carry = (DIR == kEmit) ? F2u : F1d;
-          }
-          if (i & 1) {   // the pair's 8 (step, quantity) sums: the one-lane staged reduction
-            __builtin_amdgcn_wave_barrier();
-            const int o = lane >> 3;
-            const double* t = t0 + ((o >> 2) * 4 + (o & 3)) * kStageRow + (lane & 7);
-            double y = t[0];
+        for (int i = 0; i < G; ++i) stn[i] = stale(ph, i);
 #pragma unroll
-            for (int r = 1; r < 8; ++r) y += t[8 * r];
-            y += dpp_bcast<0xB1>(y);    // quad_perm [1,0,3,2]
-            y += dpp_bcast<0x4E>(y);    // quad_perm [2,3,0,1]
-            y += dpp_bcast<0x141>(y);   // row_half_mirror
-            const int ks = k - 1 + (o >> 2);
-            if ((lane & 7) == 0 && ks < ns) red[((int64_t)sub * ns + ks) * 4 + (o & 3)] = y;
-            __builtin_amdgcn_wave_barrier();
-          }
-        }
+        for (int i = 0; i < G; ++i) step(q, i, stc[i]);
       }
       __syncthreads();
     }
+#endif
   }
   TRACE_MARK(2);
   __syncthreads();
