@@ -1385,6 +1385,9 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
 #ifndef FREI_PIPE_ROT
 #define FREI_PIPE_ROT 1
 #endif
+#ifndef FREI_PIPE_RING_AHEAD
+#define FREI_PIPE_RING_AHEAD 1
+#endif
 #ifndef FREI_PIPE_SPF   // phases ahead the consumer loads its stale fluxes (1 or 2)
 #define FREI_PIPE_SPF 1
 #endif
@@ -1545,11 +1548,11 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
     double* t0 = tile + (int64_t)sub * 2 * 4 * kStageRow;
     // step i of phase q: the carried chain, flux stores and staged bolometric terms (a pair's
     // 8 sums after its second step)
-    auto step = [&](int q, int i, double stv) {
+    // (rv: the step's psi, xi, ic, Xu, Xd, read from the ring with the rest of its phase's)
+    auto step = [&](int q, int i, double stv, const double (&rv)[kPipeNV]) {
       const int k = q * G + i;
       if (k < ns) {
-        const double psi = *rslot(q, i, 0), xi = *rslot(q, i, 1), ic = *rslot(q, i, 2);
-        const double Xu = *rslot(q, i, 3), Xd = *rslot(q, i, 4);
+        const double psi = rv[0], xi = rv[1], ic = rv[2], Xu = rv[3], Xd = rv[4];
         double F1u, F2d;
         if (DIR == kEmit) { F1u = carry; F2d = stv; } else { F2d = carry; F1u = stv; }
         const double F2u = ic * ((psi * F1u - xi * F2d) + Xu);
@@ -1590,6 +1593,17 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
         __builtin_amdgcn_wave_barrier();
       }
     };
+    // the phase's ring values, all read before its first step: one LDS round trip per phase
+    // instead of one per step on the carried chain (FREI_PIPE_RING_AHEAD 0: per step)
+    auto read_ring = [&](int q, double (&rv)[G][kPipeNV]) {
+#pragma unroll
+      for (int i = 0; i < G; ++i)
+#pragma unroll
+        for (int v = 0; v < kPipeNV; ++v) rv[i][v] = *rslot(q, i, v);
+#if FREI_PIPE_RING_AHEAD
+      __builtin_amdgcn_sched_barrier(0);   // keep the reads together, ahead of the chain
+#endif
+    };
 #if FREI_PIPE_SPF == 2
     // stale fluxes loaded two phases ahead: two register buffers (phases alternate, the loop
     // is unrolled by two), each element refilled right after its step has used it
@@ -1599,9 +1613,11 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
 #pragma unroll
     for (int i = 0; i < G; ++i) sB[i] = stale(1, i);
     auto consume = [&](int q, double (&sv)[G]) {
+      double rv[G][kPipeNV];
+      read_ring(q, rv);
 #pragma unroll
       for (int i = 0; i < G; ++i) {
-        step(q, i, sv[i]);
+        step(q, i, sv[i], rv[i]);
         sv[i] = stale(q + 2, i);
       }
     };
@@ -1629,8 +1645,10 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
         for (int i = 0; i < G; ++i) stc[i] = stn[i];
 #pragma unroll
         for (int i = 0; i < G; ++i) stn[i] = stale(ph, i);
+        double rv[G][kPipeNV];
+        read_ring(q, rv);
 #pragma unroll
-        for (int i = 0; i < G; ++i) step(q, i, stc[i]);
+        for (int i = 0; i < G; ++i) step(q, i, stc[i], rv[i]);
       }
       __syncthreads();
     }

@@ -10,7 +10,7 @@ B="python3 bench.py --no-binning --no-cpu-baseline --no-c5 --no-per-species --no
 for r in 1 2; do
   for v in ${VARIANTS:-default noprod nocons pf2}; do
     unset FREI_HIP_LIB FREI_PIPE_PF
-    case $v in noprod|nocons|nored|nostore|stalehot|spf2) export FREI_HIP_LIB=abv/$v.so;; pf2) export FREI_PIPE_PF=2;; esac
+    case $v in noprod|nocons|nored|nostore|stalehot|spf2|ring0) export FREI_HIP_LIB=abv/$v.so;; pf2) export FREI_PIPE_PF=2;; esac
     timeout -k 10 120 $B > $O/b62_${v}_$r.json 2>$O/b62_${v}_$r.err
     python3 -c "import json; d=json.load(open('$O/b62_${v}_$r.json')); print('$v', $r, '62.5k p2p', round(d['ms_per_step']*1e3,2), 'sweep', round(d['roofline']['avg_launch_ms']*1e3,2), d.get('sweep_path',{}).get('pipe'))"
   done
