@@ -74,6 +74,9 @@ SIGNATURES = {
     "frei_setup_timing": (ctypes.c_int, [_vp, _dp]),
     "frei_contract_timing": (ctypes.c_int, [_vp, _dp, _dp]),
     "frei_graph_info": (ctypes.c_int, [_vp, _ip, _ip]),
+    "frei_chain_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64)]),
+    "frei_comm_shared_device": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "frei_device_pci_bus_id": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
     "frei_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "frei_timing_read": (ctypes.c_int, [_vp, _dp, _ip]),
     "frei_timing_read_exchange": (ctypes.c_int, [_vp, _dp, _ip]),
@@ -102,8 +105,10 @@ def lib():
             raise RuntimeError(f"frei_amd: native library {LIB_PATH} is missing; build it with "
                                "`python -m frei_amd.build` (no CPU fallback exists)")
         if LIB_PATH == _DEFAULT_LIB and os.environ.get("FREI_SKIP_STAMP") != "1":
-            from .build import stamp_matches
-            if not stamp_matches(LIB_PATH):
+            from .build import sources_present, stamp_matches
+            # without the csrc sources (an installed package) the stamp cannot be verified: the
+            # library is loaded as it is; with them, a library built from other sources is refused
+            if sources_present() and not stamp_matches(LIB_PATH):
                 raise RuntimeError(f"frei_amd: {LIB_PATH} was not built from the sources in this "
                                    "tree (its .stamp hash differs); rebuild with "
                                    "`python -m frei_amd.build`")

@@ -30,9 +30,31 @@ def source_files():
             sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
 
 
+_COMPILER_ID = None
+
+
+def compiler_id():
+    """The compiler's path and its ``--version`` text (a ROCm upgrade changes the stamp)."""
+    global _COMPILER_ID
+    if _COMPILER_ID is None:
+        try:
+            out = subprocess.run([_hipcc(), "--version"], capture_output=True, text=True,
+                                 timeout=120).stdout
+        except (OSError, subprocess.SubprocessError):
+            out = "unavailable"
+        _COMPILER_ID = _hipcc() + "\n" + out
+    return _COMPILER_ID
+
+
+def sources_present():
+    return all(os.path.exists(f) for f in source_files())
+
+
 def source_hash(extra_flags=()):
-    """SHA-256 over the sources' names and bytes and the build command's flags."""
+    """SHA-256 over the sources' names and bytes, the compiler identity and the build command's
+    flags."""
     h = hashlib.sha256()
+    h.update(compiler_id().encode() + b"\0")
     for f in source_files():
         h.update(os.path.relpath(f, ROOT).encode() + b"\0")
         with open(f, "rb") as fh:

@@ -1,13 +1,18 @@
 """Mass mixing ratios (frei/chemistry.py:114-246).
 
-FastChem (``pyfastchem``, third-party C++, unpinned) is not part of this engine; like the
-reference when pyfastchem is absent (chemistry.py:142-153) the built-in mock is used:
-every species has VMR = 1.5e-3 (chemistry.py:243), mmr = VMR * mass / m_bar.  The
-engine takes per-layer mmr arrays, so a real chemistry provider can be plugged in by
-passing ``mmr=`` to :class:`frei_amd.engine.Engine` / ``Grid.load_opacities``; a provider
-whose abundances depend on temperature (FastChem's equilibrium chemistry) is passed as a
-:class:`ChemistryTable` — its output tabulated on (T, p) nodes — and the device re-evaluates
-every layer's mmr at the layer's current temperature each sweep (frei_set_chemistry).
+FastChem (``pyfastchem``, third-party C++, unpinned) is not part of this engine.  Where the
+mixing ratios come from, in order:
+
+- ``chemistry=provider``: the caller's chemistry function on the reference's signature
+  (``frei.chemistry.chemistry`` itself in the drop-in), evaluated exactly where
+  the reference's kappa evaluates it — every layer at its current (T, p), every sweep
+  (opacity.py:246-248).  A provider found independent of T (the reference's own mock) fixes
+  per-layer mixing ratios and the T-P loop stays on the device; a T-dependent one (FastChem)
+  is evaluated on the host between sweeps (Engine.run).
+- ``mmr=``: per-layer arrays, or a :class:`ChemistryTable` tabulated on (T, p) nodes that the
+  device re-interpolates at each layer's current temperature every sweep (frei_set_chemistry).
+- neither: the reference's mock (chemistry.py:142-153, 207-246): VMR = 1.5e-3 for every
+  species (chemistry.py:243), mmr = VMR * mass / m_bar.
 """
 import re
 
@@ -16,7 +21,8 @@ import numpy as np
 from .constants import AMU, M_BAR_DEFAULT
 from .units import value
 
-__all__ = ["chemistry", "iso_to_species", "iso_to_mass", "ChemistryTable"]
+__all__ = ["chemistry", "iso_to_species", "iso_to_mass", "ChemistryTable", "provider_mmr",
+           "fixed_provider_mmr"]
 
 MOCK_VMR = 1.5e-3
 
@@ -92,3 +98,56 @@ class ChemistryTable:
         if v.shape != shape:
             raise ValueError(f"chemistry table must be {shape}, got {v.shape}")
         return np.ascontiguousarray(v)
+
+
+# ------------------------------------------------------------------ chemistry providers
+# The reference's kappa calls ``chemistry(T, p, opacities.keys(), m_bar=m_bar)`` for every layer
+# of every sweep (opacity.py:246-248) — frei.chemistry.chemistry, which runs FastChem when
+# pyfastchem imports and the mock otherwise (chemistry.py:142-153).  A provider is any callable
+# on that signature returning {isotopologue: mass mixing ratio array}.  The engine takes one as
+# ``chemistry=`` (Engine, Grid.load_opacities, the emit/absorb/kappa shims) and feeds the
+# provider's own values to the opacity sum, never the built-in mock.
+
+# temperatures at which a provider is probed for T dependence: 50 K .. 10,000 K
+PROBE_T = np.geomspace(50.0, 1.0e4, 17)
+# a provider whose mixing ratios move by less than this (relative) over PROBE_T is taken as
+# T-independent: the reference's own mock returns 1.5e-3 n/n, equal to an ulp or two
+PROBE_RTOL = 1e-12
+
+
+def provider_mmr(provider, temperatures, pressures_bar, species, m_bar):
+    """Mass mixing ratios [n_species][n] of ``provider`` at the points (T[i], p[i]), called as
+    the reference calls its chemistry (opacity.py:246-248): temperatures in K and pressures in
+    bar as astropy Quantities when astropy is importable (the reference's own environment),
+    plain arrays otherwise; ``m_bar`` in g likewise."""
+    T = np.atleast_1d(np.asarray(temperatures, dtype=np.float64))
+    p = np.atleast_1d(np.asarray(pressures_bar, dtype=np.float64))
+    try:
+        import astropy.units as u
+        args, mb = (T * u.K, p * u.bar), float(m_bar) * u.g
+    except ImportError:
+        args, mb = (T, p), float(m_bar)
+    out = provider(*args, list(species), m_bar=mb)
+    rows = []
+    for iso in species:
+        if iso not in out:
+            raise KeyError(f"chemistry provider returned no mixing ratio for {iso!r} "
+                           "(the reference's kappa would fail the same way)")
+        v = out[iso]
+        v = getattr(v, "value", v)            # a dimensionless Quantity
+        rows.append(np.broadcast_to(np.asarray(v, dtype=np.float64), T.shape))
+    return np.array(rows)
+
+
+def fixed_provider_mmr(provider, species, pressures_bar, m_bar, temperatures=PROBE_T,
+                       rtol=PROBE_RTOL):
+    """[n_species][n_layers] when ``provider`` does not depend on temperature at the layer
+    pressures (probed at ``temperatures``, relative spread <= ``rtol``), else None."""
+    p = np.asarray(pressures_bar, dtype=np.float64)
+    T = np.asarray(temperatures, dtype=np.float64)
+    v = provider_mmr(provider, np.repeat(T, p.size), np.tile(p, T.size), species, m_bar)
+    v = v.reshape(len(species), T.size, p.size)
+    ref = v[:, T.size // 2, :]
+    if np.all(np.abs(v - ref[:, None, :]) <= rtol * np.abs(ref[:, None, :])):
+        return np.ascontiguousarray(ref)
+    return None

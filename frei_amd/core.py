@@ -93,6 +93,7 @@ class Grid:
             self.init_temperatures = np.asarray(value(init_temperatures, "K"), dtype=float)
         self.opacities = None
         self.mmr = None
+        self.chemistry = None
         self.device = device
         self._engine = None
         self._last_dtaus = None
@@ -103,12 +104,16 @@ class Grid:
                 f"lam=[{self.lam[0]}...{self.lam[-1]}] um>")
 
     def load_opacities(self, species=None, path=None, opacities=None, client=None,
-                       force_reload=False, groupies=False, mmr=None, cross_sections=None):
+                       force_reload=False, groupies=False, mmr=None, cross_sections=None,
+                       chemistry=None):
         """Attach opacity tables (core.py:198-231).  ``opacities`` is the reference's dict
         of (pressure, temperature, wavelength) tables; otherwise high-resolution
         cross-sections (files at ``path`` or ``cross_sections``) are binned on the GPU
-        straight into the engine's tables (opacity.py:66-170).  ``mmr`` optionally
-        overrides the mock chemistry with per-species, per-layer mass mixing ratios."""
+        straight into the engine's tables (opacity.py:66-170).  The mixing ratios come from
+        ``chemistry`` — a provider on the reference's ``chemistry(T, p, species, m_bar=...)``
+        signature, called wherever the reference's kappa calls it (opacity.py:246-248; the
+        drop-in passes frei's own) — or ``mmr`` (per-species, per-layer
+        arrays or a ChemistryTable); with neither, the reference's mock."""
         if (self.opacities is None and opacities is None) or force_reload:
             from .binning import binned_opacity
             self.opacities = binned_opacity(self.init_temperatures, self.pressures,
@@ -117,7 +122,10 @@ class Grid:
                                             cross_sections=cross_sections, device=self.device)
         else:
             self.opacities = opacities
+        if mmr is not None and chemistry is not None:
+            raise ValueError("pass either mmr or a chemistry provider, not both")
         self.mmr = mmr
+        self.chemistry = chemistry
         self._close_engine()
         return self.opacities
 
@@ -133,7 +141,7 @@ class Grid:
             self._engine = Engine(self.lam, self.pressures, self.opacities, g=pl.g,
                                   m_bar=pl.m_bar,
                                   F_toa=F_TOA(self.lam, T_star=pl.T_star, a_rstar=pl.a_rstar),
-                                  mmr=self.mmr, device=self.device)
+                                  mmr=self.mmr, chemistry=self.chemistry, device=self.device)
         return self._engine
 
     def emission_spectrum(self, n_timesteps=1, n_zero_crossings=2, convergence_dT=3.0):

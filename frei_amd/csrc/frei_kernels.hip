@@ -28,24 +28,30 @@ namespace frei {
 // FREI_TRACE builds only (tools/trace_probe.py): thread 0 of every block of the sweeps and
 // the fused update appends (kernel kind, block, 4 wall-clock marks at 100 MHz) to a device
 // ring — entry, end of the prologue, end of the main loop, exit — so one T-P half-iteration's
-// launch latency, prologue, steps and drain can be read off without a profiler.
+// launch latency, prologue, steps and drain can be read off without a profiler.  Beside the
+// wall clock, entry and exit also stamp the shader-cycle counter (s_memtime): Δcycles ÷
+// Δwall × 100 MHz is the clock the block ran at (MI355X_MICROARCH.md, DVFS item 6).
 #ifdef FREI_TRACE
 struct TraceRec {
-  long long kind, block, t[4];
+  long long kind, block, t[4], cyc[2];
 };
 constexpr unsigned kTraceCap = 1u << 17;
 __device__ TraceRec g_trace[kTraceCap];
 __device__ unsigned int g_trace_n;
-#define TRACE_DECL long long tr_[4] = {wall_clock64(), 0, 0, 0}
+#define TRACE_DECL                                                           \
+  long long tr_[4] = {wall_clock64(), 0, 0, 0};                              \
+  const long long trc_ = (long long)__builtin_amdgcn_s_memtime()
 #define TRACE_MARK(i) (tr_[i] = wall_clock64())
 #define TRACE_PUT(kind)                                                      \
   do {                                                                       \
     tr_[3] = wall_clock64();                                                 \
+    const long long trc1_ = (long long)__builtin_amdgcn_s_memtime();         \
     if (threadIdx.x == 0) {                                                  \
       const unsigned i_ = atomicAdd(&g_trace_n, 1u);                         \
       if (i_ < kTraceCap)                                                    \
         g_trace[i_] = TraceRec{(kind), (long long)blockIdx.x,                \
-                               {tr_[0], tr_[1], tr_[2], tr_[3]}};            \
+                               {tr_[0], tr_[1], tr_[2], tr_[3]},             \
+                               {trc_, trc1_}};                               \
     }                                                                        \
   } while (0)
 #else
@@ -3172,8 +3178,9 @@ void launch_fill(double* x, int64_t n, double v, hipStream_t st) {
 }  // namespace frei
 
 #ifdef FREI_TRACE
-// Diagnostic builds only: copy out (and reset) the trace ring.  rec: n_max x 6 int64
-// (kind, block, 4 wall-clock marks); *n: records written since the last reset.
+// Diagnostic builds only: copy out (and reset) the trace ring.  rec: n_max x 8 int64
+// (kind, block, 4 wall-clock marks, 2 shader-cycle stamps at entry and exit); *n: records
+// written since the last reset.
 extern "C" int frei_trace_fetch(long long* rec, int n_max, int* n) {
   unsigned cnt = 0;
   if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(frei::g_trace_n), sizeof(cnt)) != hipSuccess) return -1;

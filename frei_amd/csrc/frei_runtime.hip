@@ -134,6 +134,8 @@ struct frei_ctx {
   hipGraphExec_t g_exec = nullptr;
   std::vector<uint64_t> g_key;
   int g_captures = 0, g_replays = 0;     // frei_graph_info
+  int64_t n_chained = 0;                // chained sweep launches so far (frei_chain_info)
+  bool shared_device = false;           // ranks share this GPU: no chained launches
   std::vector<uint64_t>* keys = nullptr;  // collecting run_sweep's argument hashes
   bool dry = false;                       // run_sweep computes hashes only (no launches)
   // tables
@@ -649,9 +651,15 @@ bool fused_ok(frei_ctx* c) {
 // This sweep can run chained: a grouped-lane or one-lane (two or more steps in flight) sweep
 // of the contracted table forming its own step records, fused update, stream launches (no graph
 // capture).
+// Not while per-sweep HIP events are on (frei_timing): events around a chained launch would also
+// cover the deferred update it runs, including its wait for the peers' sums, so a timed run
+// launches sweep and update separately and the events time the sweep alone.  Not when ranks
+// share this device (frei_comm_shared_device): a chained launch's sweep blocks
+// spin on the update workgroups, which wait for every rank's sums, and could hold the CUs
+// another rank's kernels need.
 bool chain_ready(frei_ctx* c) {
   if (!(c->chain && c->fast && c->eff && c->shared && records_in_sweep(c) && fused_ok(c) &&
-        !c->use_graph && !c->keys))
+        !c->use_graph && !c->keys && !c->timing && !c->shared_device))
     return false;
   const int nc = pipe_consumers(c);
   // producer/consumer, four consumers per block; the chained kernel adds the update body's
@@ -808,6 +816,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
       u.epoch_val = c->chain_seq;
       c->has_pend = false;
       launch_sweep_pipe_chain(o.dir, c->pipe_pf, f, u, nb_run, c->stream);
+      ++c->n_chained;
     } else if (NC > 0) {
       launch_sweep_pipe(o.dir, NC, c->pipe_pf, f, nb_run, c->stream);
     } else if (Q > 1 && merge) {
@@ -816,6 +825,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
       u.epoch_val = c->chain_seq;
       c->has_pend = false;
       launch_sweep_chain(o.dir, Q, NW, f, u, nb_run, c->stream);
+      ++c->n_chained;
     } else if (Q > 1) {
       launch_sweep_group(o.dir, Q, NW, f, nb_run, c->stream);
     } else if (merge) {   // the one-lane contracted sweep, records formed in the block
@@ -824,6 +834,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
       u.epoch_val = c->chain_seq;
       c->has_pend = false;
       launch_sweep_fast_chain(o.dir, depth, pf, f, u, c->nblocks, c->stream);
+      ++c->n_chained;
     } else {
       launch_sweep_fast(o.dir, S_run, depth, pf, nan_check && !c->eff, c->shared != 0, f,
                         c->nblocks, c->stream);
@@ -1041,7 +1052,11 @@ int check_comm(frei_ctx* c) {
   if (c->d_chain_err) {
     int e = 0;
     HIP_TRY(hipMemcpy(&e, c->d_chain_err, sizeof(int), hipMemcpyDeviceToHost));
-    if (e) return fail("chained sweep: the update workgroups never published the temperatures");
+    if (e) {   // reported once: rearm it so later runs on this context are not failed by it
+      c->has_pend = false;
+      HIP_TRY(hipMemset(c->d_chain_err, 0, sizeof(int)));
+      return fail("chained sweep: the update workgroups never published the temperatures");
+    }
   }
   if (!c->d_comm_err) return 0;
   int e = 0;
@@ -1534,6 +1549,7 @@ int frei_state_init(frei_ctx* c, const double* T_init) {
   if (!ready(c) || !T_init) return fail("context not ready or null T_init");
   TRY(set_device(c));
   TRY(build_meta(c));
+  c->has_pend = false;   // an update deferred by an interrupted run must not land on the new T
   home_temperatures(c);
   TRY(h2d(c->d_T, T_init, (size_t)c->nL * c->n_atm, c->stream));
   const size_t F = (size_t)c->nL * c->nlam * c->n_atm;
@@ -1545,7 +1561,17 @@ int frei_state_init(frei_ctx* c, const double* T_init) {
   return 0;
 }
 
+static int iterate_steps(frei_ctx* c, int n, int nzc, double thr, double alpha, bool stop);
+
+// An error part-way leaves no update deferred: a later frei_state_init + sweep must not flush a
+// stale one over the freshly uploaded temperatures.
 static int iterate_direct(frei_ctx* c, int n, int nzc, double thr, double alpha, bool stop) {
+  const int rc = iterate_steps(c, n, nzc, thr, alpha, stop);
+  if (rc != 0) c->has_pend = false;
+  return rc;
+}
+
+static int iterate_steps(frei_ctx* c, int n, int nzc, double thr, double alpha, bool stop) {
   for (int it = 0; it < n; ++it) {
     SweepOpts e;
     e.dir = kEmit;
@@ -1631,6 +1657,24 @@ int frei_graph_info(frei_ctx* c, int* captures, int* replays) {
   if (!c) return fail("null argument");
   if (captures) *captures = c->g_captures;
   if (replays) *replays = c->g_replays;
+  return 0;
+}
+
+int frei_comm_shared_device(frei_ctx* c, int shared) {
+  if (!c) return fail("null argument");
+  c->shared_device = shared != 0;
+  return 0;
+}
+
+int frei_device_pci_bus_id(int device, char* buf, int len) {
+  if (!buf || len < 16) return fail("null argument or buffer under 16 bytes");
+  HIP_TRY(hipDeviceGetPCIBusId(buf, len, device));
+  return 0;
+}
+
+int frei_chain_info(frei_ctx* c, int64_t* chained) {
+  if (!c || !chained) return fail("null argument");
+  *chained = c->n_chained;
   return 0;
 }
 

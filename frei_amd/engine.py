@@ -14,7 +14,8 @@ import numpy as np
 
 from . import _native as N
 from .binning import BinnedTable
-from .chemistry import ChemistryTable, chemistry
+from .chemistry import ChemistryTable, fixed_provider_mmr, provider_mmr
+from .chemistry import chemistry as mock_chemistry
 from .constants import BAR, C, H, K_B, M_BAR_DEFAULT, UM
 from .opacity import SeparableTable, sigma_scattering, table_values
 from .units import scalar, value
@@ -86,6 +87,14 @@ def _table_arrays(tab):
     return p, T
 
 
+def device_key(device):
+    """Host name and PCI bus id of ``device``: equal for ranks that share one GPU."""
+    import socket
+    buf = ctypes.create_string_buffer(64)
+    N.check(N.lib().frei_device_pci_bus_id(int(device), buf, 64))
+    return f"{socket.gethostname()}|{buf.value.decode()}"
+
+
 class Engine:
     """One device context for the wavelength slice ``lam_slice`` of ``lam_um``.
 
@@ -93,11 +102,14 @@ class Engine:
     descending), ``opacities`` dict of tables, ``g`` (cm s^-2), ``m_bar`` (g),
     ``F_toa`` (erg s^-1 cm^-3, global grid) and ``mmr`` [n_species][n_layers]
     (default: the reference's mock chemistry, chemistry.py:207-246) or a
-    :class:`~frei_amd.chemistry.ChemistryTable` (T-dependent, re-evaluated every sweep).
+    :class:`~frei_amd.chemistry.ChemistryTable` (T-dependent, re-evaluated every sweep), or
+    ``chemistry``: a provider on the reference's signature ``chemistry(T, p, species,
+    m_bar=...)`` (frei_amd.chemistry, "chemistry providers"), evaluated where the reference's
+    kappa evaluates it.
     """
 
     def __init__(self, lam_um, p_bar, opacities, g=2478.6519476149147, m_bar=M_BAR_DEFAULT,
-                 F_toa=None, mmr=None, device=0, lam_slice=None, comm=None):
+                 F_toa=None, mmr=None, device=0, lam_slice=None, comm=None, chemistry=None):
         lib = N.lib()
         self.lam_um = np.asarray(value(lam_um, "um"), dtype=float)
         self.p_bar = np.asarray(value(p_bar, "bar"), dtype=float)
@@ -128,10 +140,22 @@ class Engine:
                                   self.g, self.m_bar))
         for s, name in enumerate(self.names):
             self._set_table(s, opacities[name], sl)
+        # a chemistry provider (the reference's chemistry(T, p, species, m_bar)): fixed per-layer
+        # mixing ratios when it does not depend on T, else evaluated between sweeps (run)
+        self.provider = None
+        provider = chemistry
+        if provider is not None:
+            if mmr is not None:
+                raise ValueError("pass either mmr or a chemistry provider, not both")
+            mmr = fixed_provider_mmr(provider, self.names, self.p_bar, self.m_bar)
+            if mmr is None:
+                self.provider = provider
+                mmr = provider_mmr(provider, np.full(self.n_layers, 1000.0), self.p_bar,
+                                   self.names, self.m_bar)
         chem = mmr if isinstance(mmr, ChemistryTable) else None
         if mmr is None or chem is not None:
             T0 = np.full(self.n_layers, 1000.0)
-            mm = chemistry(T0, self.p_bar, self.names, m_bar=self.m_bar)
+            mm = mock_chemistry(T0, self.p_bar, self.names, m_bar=self.m_bar)
             mmr = np.array([mm[nm] for nm in self.names])
         self.mmr = N.f64(np.broadcast_to(np.asarray(mmr, dtype=float),
                                          (len(self.names), self.n_layers)))
@@ -143,6 +167,10 @@ class Engine:
                                            chem.temperature.size,
                                            N.dptr(N.f64(chem.pressure * BAR)),
                                            chem.pressure.size))
+        if self.provider is not None:
+            # mixing ratios change every sweep: the per-species sum in the sweep (the reference's
+            # own order) instead of a species contraction rebuilt per sweep
+            self.set_option("precontract", 0)
         self._ag_keep = None
         if comm is not None:
             self._join(comm)
@@ -170,6 +198,11 @@ class Engine:
                 raise RuntimeError(f"frei_hip: {msg}")
             if len(hs) != nranks or any(len(x) != 64 for x in hs):
                 raise RuntimeError("P2P setup failed on a peer rank (no mailbox handle)")
+            # ranks on one GPU (the one-GPU rehearsal): no chained launches on this context
+            # (every rank joins this exchange before any can fail in p2p_open)
+            me = device_key(self.device).encode()
+            if arg(me).count(me) > 1 and os.environ.get("FREI_CHAIN_SHARED") != "1":
+                N.check(lib.frei_comm_shared_device(self._ctx, 1))
             allh = ctypes.create_string_buffer(b"".join(hs), 64 * nranks)
             N.check(lib.frei_comm_p2p_open(self._ctx, allh))
         elif kind == "host":
@@ -253,9 +286,18 @@ class Engine:
                                    N.dptr(dtaus)))
         return dT, bol, dtaus
 
+    def set_mmr(self, mmr):
+        """Per-layer mass mixing ratios [n_species][n_layers] for the following sweeps."""
+        self.mmr = N.f64(np.broadcast_to(np.asarray(mmr, dtype=float),
+                                         (len(self.names), self.n_layers)))
+        N.check(N.lib().frei_set_mmr(self._ctx, N.dptr(self.mmr)))
+
     def run(self, T_init, n_timesteps=1, n_zero_crossings=2, convergence_dT=3.0, alpha=1.0,
             want_dtaus=True):
         """Grid.emission_spectrum on the device (core.py:233-338)."""
+        if self.provider is not None:
+            return self._run_provider(T_init, n_timesteps, n_zero_crossings, convergence_dT,
+                                      alpha, want_dtaus)
         nL = self.n_layers
         n_iter = ctypes.c_int(0)
         T_final = np.empty(nL)
@@ -269,6 +311,45 @@ class Engine:
         it = n_iter.value
         temp_hist = hist[: nL * 2 * it].reshape(nL, 2 * it)
         return dict(spectrum=spec, final_T=T_final, temp_hist=temp_hist, dtaus=dtaus, n_iter=it)
+
+    def _provider_step(self, T):
+        """The provider's mixing ratios at every layer's (T, p), as kappa's chemistry call
+        (opacity.py:246-248) sees them in the coming sweep."""
+        self.set_mmr(provider_mmr(self.provider, T, self.p_bar, self.names, self.m_bar))
+
+    def _run_provider(self, T_init, n_timesteps, n_zero_crossings, convergence_dT, alpha,
+                      want_dtaus):
+        """core.py:264-338 stepped from the host for a T-dependent chemistry provider: before
+        every sweep the provider runs at the layers' current temperatures (read back from the
+        device, 8 B per layer) and its mixing ratios go up; the sweeps, bolometric sums and T
+        updates run on the device as in :meth:`run`.  The convergence test is core.py:301-318's
+        (Q13) on the absorb sweeps' histories."""
+        nL = self.n_layers
+        self.state_init(T_init)              # zero fluxes (core.py:265-266), T = T_init
+        T = self.get_temperatures()
+        hists = []
+        it = 0
+        for it in range(1, int(n_timesteps) + 1):
+            self._provider_step(T)
+            self.sweep(EMIT, alpha=alpha, want_dtaus=False)
+            T1 = self.get_temperatures()
+            self._provider_step(T1)
+            dT, _, _ = self.sweep(ABSORB, alpha=alpha, want_dtaus=False)
+            T = self.get_temperatures()
+            hists.append(np.stack([T1, T], axis=1))
+            th = np.hstack(hists)
+            th = th.T[th[0] != 0].T
+            diffs = np.diff(th.T, axis=0)
+            conv = ((np.count_nonzero(np.sign(diffs[1:]) != np.sign(diffs[:-1]), axis=0)
+                     > n_zero_crossings) | (np.abs(dT) < convergence_dT))
+            if np.all(conv):
+                break
+        self._provider_step(T)
+        _, _, dtaus = self.sweep(EMIT, alpha=1.0, want_dtaus=want_dtaus)   # Q7: alpha = 1
+        up, _ = self.get_fluxes()
+        return dict(spectrum=up[-1].copy(), final_T=self.get_temperatures(),
+                    temp_hist=np.hstack(hists) if hists else np.empty((nL, 0)),
+                    dtaus=dtaus, n_iter=it)
 
     def state_init(self, T_init):
         N.check(N.lib().frei_state_init(self._ctx, N.dptr(N.f64(T_init))))
@@ -336,6 +417,13 @@ class Engine:
         N.check(N.lib().frei_graph_info(self._ctx, ctypes.byref(cap), ctypes.byref(rep)))
         return cap.value, rep.value
 
+    def chain_count(self):
+        """Chained sweep launches so far (frei_chain_info): sweeps whose launch also ran the
+        previous sweep's deferred update."""
+        n = ctypes.c_int64(0)
+        N.check(N.lib().frei_chain_info(self._ctx, ctypes.byref(n)))
+        return n.value
+
     def setup_timing(self):
         """Milliseconds of the last one-time metadata build by phase (frei_setup_timing)."""
         ms = np.zeros(5)
@@ -384,19 +472,23 @@ def _tables_key(opacities):
     return (id(opacities), tuple(out))
 
 
-def cached_engine(opacities, *, lam_um, p_bar, g, m_bar, F_toa, mmr=None, device=0):
+def cached_engine(opacities, *, lam_um, p_bar, g, m_bar, F_toa, mmr=None, device=0,
+                  chemistry=None, tag=None):
     """An :class:`Engine` for these tables and grid, reused across calls with the same
-    opacity dict (by identity) and equal grid arrays / scalars."""
+    opacity dict (by identity), equal grid arrays / scalars and the same chemistry provider
+    (by identity); ``tag`` separates contexts whose mixing ratios a caller sets itself."""
     key = (_tables_key(opacities), _array_key(lam_um), _array_key(p_bar), float(g),
            float(m_bar), None if F_toa is None else _array_key(F_toa),
-           None if mmr is None else _array_key(mmr), int(device))
+           None if mmr is None else _array_key(mmr), int(device),
+           None if chemistry is None else id(chemistry), tag)
     for i, (k, _, eng) in enumerate(_ENGINE_CACHE):
         if k == key and eng._ctx:
             _ENGINE_CACHE.insert(0, _ENGINE_CACHE.pop(i))
             return eng
     eng = Engine(lam_um, p_bar, opacities, g=g, m_bar=m_bar, F_toa=F_toa, mmr=mmr,
-                 device=device)
-    _ENGINE_CACHE.insert(0, (key, (opacities, tuple(opacities.values())), eng))
+                 device=device, chemistry=chemistry)
+    # the provider is kept alive with the entry, so its id stays unique while cached
+    _ENGINE_CACHE.insert(0, (key, (opacities, tuple(opacities.values()), chemistry, tag), eng))
     while len(_ENGINE_CACHE) > _ENGINE_CACHE_SIZE:
         _ENGINE_CACHE.pop()[2].close()
     return eng

@@ -142,21 +142,34 @@ def sigma_scattering(lam_um, m_bar):
 _KAPPA_P = np.array([4.0, 2.0, 1.0, 0.5])   # bar: kappa's context needs some layer grid
 
 
-def kappa(opacities, temperature, pressure, lam, m_bar=M_BAR_DEFAULT, device=0):
+def kappa(opacities, temperature, pressure, lam, m_bar=M_BAR_DEFAULT, device=0,
+          chemistry=None):
     """Total opacity at one (T, p): (k, sigma_scattering) in cm^2 g^-1 (opacity.py:203-269).
 
     k = sum_s mmr_s * interp_s(p, T) + sigma (linear, fill 0 outside the node hull;
-    pressure-only for single-temperature tables).  Runs on the GPU."""
+    pressure-only for single-temperature tables).  mmr_s = ``chemistry(T, p, species,
+    m_bar=m_bar)`` at the query point (opacity.py:246-248) when a provider is given, else the
+    reference's mock.  Runs on the GPU."""
+    from .chemistry import provider_mmr
     from .engine import cached_engine
     lam_um = np.asarray(value(lam, "um"), dtype=float)
     T = np.asarray(value(temperature, "K"), dtype=float)
     p = np.asarray(value(pressure, "bar"), dtype=float)
+    mb = scalar(m_bar, "g")
     # one context per (tables, wavelengths, m_bar), reused across calls; its layer grid only
-    # carries the mock chemistry's (layer-independent) mixing ratios
-    eng = cached_engine(opacities, lam_um=lam_um, p_bar=_KAPPA_P, g=1.0,
-                        m_bar=scalar(m_bar, "g"), F_toa=None, device=device)
+    # carries the mixing ratios: the mock's (layer-independent), or the provider's at each
+    # query point, set before the query
+    eng = cached_engine(opacities, lam_um=lam_um, p_bar=_KAPPA_P, g=1.0, m_bar=mb, F_toa=None,
+                        device=device, tag=None if chemistry is None else ("kappa", id(chemistry)))
+    names = list(opacities)
+
+    def query(Tq, pq):
+        if chemistry is not None:
+            m = provider_mmr(chemistry, [Tq], [pq], names, mb)[:, 0]
+            eng.set_mmr(np.repeat(m[:, None], _KAPPA_P.size, axis=1))
+        return eng.kappa(Tq, pq)
     if T.ndim == 0 and p.ndim == 0:
-        return eng.kappa(float(T), float(p))
+        return query(float(T), float(p))
     # vector mode: points along one dimension z (opacity.py:235-263).  The reference
     # flattens the (z, lam) result before adding sigma (opacity.py:266-269), so a one-point
     # array gives a flat k; for z > 1 its broadcast fails, and here k is (z, lam).
@@ -164,7 +177,7 @@ def kappa(opacities, temperature, pressure, lam, m_bar=M_BAR_DEFAULT, device=0):
     ks = []
     sig = None
     for Tq, pq in zip(Tz.ravel(), pz.ravel()):
-        k, sig = eng.kappa(float(Tq), float(pq))
+        k, sig = query(float(Tq), float(pq))
         ks.append(k)
     if len(ks) == 1:
         return ks[0], sig

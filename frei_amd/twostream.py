@@ -46,7 +46,7 @@ def propagate_fluxes(lam, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0=0, g_0=
 
 
 def _sweeps(direction, opacities, temperatures, pressures, lam, F_TOA, g, m_bar, n_timesteps,
-            convergence_thresh, alpha, fluxes_up, fluxes_down, device):
+            convergence_thresh, alpha, fluxes_up, fluxes_down, device, chemistry=None):
     T = np.array(value(temperatures, "K"), dtype=float)
     p = np.asarray(value(pressures, "bar"), dtype=float)
     lam_um = np.asarray(value(lam, "um"), dtype=float)
@@ -55,7 +55,8 @@ def _sweeps(direction, opacities, temperatures, pressures, lam, F_TOA, g, m_bar,
     thresh = scalar(convergence_thresh, "K")
     # the context (uploaded tables) is reused by later calls with the same opacity dict
     eng = cached_engine(opacities, lam_um=lam_um, p_bar=p, g=scalar(g, "cm / s2"),
-                        m_bar=scalar(m_bar, "g"), F_toa=ftoa, device=device)
+                        m_bar=scalar(m_bar, "g"), F_toa=ftoa, device=device,
+                        chemistry=chemistry)
     up_in, down_in = fluxes_up, fluxes_down
     up = np.zeros((nL, nlam)) if up_in is None else np.array(value(up_in, "erg / (s cm3)"))
     down = (np.zeros((nL, nlam)) if down_in is None
@@ -70,6 +71,8 @@ def _sweeps(direction, opacities, temperatures, pressures, lam, F_TOA, g, m_bar,
     dtaus = dT = None
     for j in range(n_timesteps):
         eng.set_temperatures(hist[:, j])
+        if eng.provider is not None:   # kappa's chemistry call at this sweep's T (opacity.py:246)
+            eng._provider_step(hist[:, j])
         dT, _, dtaus = eng.sweep(direction, alpha=alpha)
         hist[:, j + 1] = hist[:, j] - dT
         if n_timesteps > 1 and np.abs(dT).max() < thresh:
@@ -87,16 +90,18 @@ def _sweeps(direction, opacities, temperatures, pressures, lam, F_TOA, g, m_bar,
 
 def emit(opacities, temperatures, pressures, lam, F_TOA, g, m_bar=M_BAR_DEFAULT,
          n_timesteps=50, convergence_thresh=10.0, alpha=1, fluxes_up=None, fluxes_down=None,
-         device=0):
+         device=0, chemistry=None):
     """Upward sweep(s) (twostream.py:290-421) ->
-    (fluxes_up, fluxes_down, final_temps, temperature_history, dtaus, dT)."""
+    (fluxes_up, fluxes_down, final_temps, temperature_history, dtaus, dT).  ``chemistry``:
+    the mixing-ratio provider kappa calls (opacity.py:246-248; default the reference's mock)."""
     return _sweeps(EMIT, opacities, temperatures, pressures, lam, F_TOA, g, m_bar, n_timesteps,
-                   convergence_thresh, alpha, fluxes_up, fluxes_down, device)
+                   convergence_thresh, alpha, fluxes_up, fluxes_down, device, chemistry)
 
 
 def absorb(opacities, temperatures, pressures, lam, F_TOA, g, m_bar=M_BAR_DEFAULT,
            n_timesteps=50, convergence_thresh=10.0, alpha=1, fluxes_up=None, fluxes_down=None,
-           device=0):
+           device=0, chemistry=None):
     """Downward sweep(s) (twostream.py:424-550), same returns as :func:`emit`."""
     return _sweeps(ABSORB, opacities, temperatures, pressures, lam, F_TOA, g, m_bar,
-                   n_timesteps, convergence_thresh, alpha, fluxes_up, fluxes_down, device)
+                   n_timesteps, convergence_thresh, alpha, fluxes_up, fluxes_down, device,
+                   chemistry)

@@ -232,6 +232,17 @@ int frei_set_option(frei_ctx* ctx, const char* name, int value);
  * replayed from a captured hipGraph of a few iterations when one rank runs with timing off:
  * the number of captures and of graph launches so far. */
 int frei_graph_info(frei_ctx* ctx, int* captures, int* replays);
+/* Chained sweep launches so far (FREI_CHAIN / option "chain": a sweep launch whose leading
+ * workgroups run the previous sweep's deferred fused update).  Never while per-sweep HIP events
+ * are on (frei_timing) or when P2P ranks share this device. */
+int frei_chain_info(frei_ctx* ctx, int64_t* chained);
+/* Ranks of this communicator share the context's GPU (shared != 0): no chained launches (a
+ * chained launch's sweep blocks spin on update workgroups that wait for every rank's sums, and
+ * could hold the CUs another rank's kernels need).  frei_amd sets it when two ranks report the
+ * same host and PCI bus id (frei_device_pci_bus_id). */
+int frei_comm_shared_device(frei_ctx* ctx, int shared);
+/* The PCI bus id string of a device ("0000:05:00.0"), len >= 16. */
+int frei_device_pci_bus_id(int device, char* buf, int len);
 /* Host wall-clock milliseconds of the last metadata build (the one-time setup before the
  * first sweep after tables/mmr change), by phase: [0] per-(species, layer) brackets on the
  * host, [1] metadata uploads, [2] contracted-table allocation, [3] its zero fill, [4] the K3

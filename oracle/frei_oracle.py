@@ -220,23 +220,30 @@ def _localized(coords, x):
     return c[sl], order[sl]
 
 
+def _table_row(values, pi, ti):
+    """values[pi, ti, :] — for a lazy SeparableValues only that row is formed (same arithmetic,
+    elementwise, as the whole table)."""
+    if isinstance(values, SeparableValues):
+        return values.row(pi, ti)
+    return values[pi, ti]
+
+
 def interp_table(tab, T, p_bar):
     """xarray DataArray.interp(pressure, [temperature], linear, fill 0) at one point
     (opacity.py:250-263): interpn for 2-D, interp1d for the single-T case."""
     pc, pidx = _localized(tab.pressure, p_bar)
-    vals = tab.values[pidx]
     if len(np.unique(tab.temperature)) > 1:
         tc, tidx = _localized(tab.temperature, T)
-        vals = vals[:, tidx]
         ip, yp, oobp = _bracket(pc, p_bar)
         it, yt, oobt = _bracket(tc, T)
         if oobp or oobt:
-            return np.zeros(vals.shape[-1])
+            return np.zeros(tab.values.shape[-1])
         out = 0.
         for a, wa in ((ip, 1 - yp), (ip + 1, yp)):
             for b, wb in ((it, 1 - yt), (it + 1, yt)):
-                out = out + vals[a, b] * (1. * wa * wb)
+                out = out + _table_row(tab.values, pidx[a], tidx[b]) * (1. * wa * wb)
         return out
+    vals = tab.values[pidx]
     # single unique temperature: scipy interp1d linear over pressure
     if p_bar < pc[0] or p_bar > pc[-1]:
         return np.zeros(vals.shape[-1])
@@ -531,6 +538,10 @@ class SeparableValues:
         fp = self.fp[pidx]
         return np.clip((fp[:, None] * self.fT[None, :])[:, :, None] * self.base[None, None, :],
                        self.lo, self.hi)
+
+    def row(self, pi, ti):
+        """self[pi][ti]: clip((fp[pi] fT[ti]) base) — the same operations in the same order."""
+        return np.clip((self.fp[pi] * self.fT[ti]) * self.base, self.lo, self.hi)
 
 
 # ----------------------------------------------------------------- opacity binning (§8(f) #1)

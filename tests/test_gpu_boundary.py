@@ -1,8 +1,16 @@
 """GPU side of the opacity-table boundary: the reference's own binned tables, handed over as
 DataArray-like objects in the layouts the reference produces, must give the same emission
 spectrum as the (pressure, temperature, wavelength) form — bit for bit, since the engine sees
-identical tables — and match the oracle.  n_T = n_p on the Grid (6 layers), so a transpose
-could not hide behind a shape check (VERDICT r02 "what's missing" #1)."""
+identical tables — and match the oracle.  n_T = n_p on the Grid (6 and 10 layers), so a
+transpose could not hide behind a shape check (VERDICT r02 "what's missing" #1).
+
+The 6-layer groupies table is the reference's trapz x bin width x 1e-3 (interp.py:287-307):
+median 4.5e-5 cm^2/g on that cross-section, a nearly transparent atmosphere whose thin layers
+(dtau ~ 1e-8) turn one ulp of exp into ~1e-6 of the emergent spectrum — its one-ulp floor
+(4.5e-6) is the reference's own reproducibility there, not slack.  The 10-layer case
+(binning_g3.npz, make_binning_goldens.py strong()) is the same line forest at 1e5 x strength,
+binned by the reference: floor 2.5e-11, so it is held to 1e-10 outright, and its swapped-dims
+control must miss by more than 1e-4."""
 import numpy as np
 import pytest
 
@@ -15,9 +23,9 @@ pytestmark = pytest.mark.gpu
 G_J, M_BAR = 2478.6519476149147, 4.0142926168559996e-24
 
 
-def _run(fa, B, tabs, n=3):
-    grid = fa.Grid(fa.Planet.from_hot_jupiter(), lam=B["g1_lam"], pressures=B["g1_p"],
-                   init_temperatures=B["g1_T"])
+def _run(fa, B, tabs, n=3, g="g1"):
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), lam=B[g + "_lam"], pressures=B[g + "_p"],
+                   init_temperatures=B[g + "_T"])
     grid.load_opacities(opacities=tabs)
     spec, T, th, dtaus = grid.emission_spectrum(n_timesteps=n)
     up, down = grid.engine().get_fluxes()
@@ -67,3 +75,36 @@ def test_reference_binned_tables_drop_in_by_dimension_name(golden, mode):
     _, s_sw, T_sw, _, _ = _run(fa, B, swapped)
     assert not np.array_equal(T_sw, T_ref)
     assert float(np.max(np.abs(s_sw - s_ref) / np.abs(s_ref))) > 1e-6
+
+
+def test_reference_binned_strong_table_at_1e10(golden):
+    """The reference's groupies table of a well-conditioned atmosphere (binning_g3.npz), handed
+    over as (temperature, pressure, wavelength) DataArray: 1e-10 without any floor widening
+    (the measured one-ulp floor must itself be below 1e-10), and p/T swapped misses by > 1e-4."""
+    import frei_amd as fa
+    B = golden("binning_g3.npz")
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), n_layers=10, T_ref=2400)
+    assert np.allclose(grid.init_temperatures, B["g3_T"], rtol=1e-13)
+    assert np.allclose(grid.pressures, B["g3_p"], rtol=1e-13)
+    raw = B["g3_groupies"]
+    assert raw.shape == (10, 10, 500) and np.median(raw) > 1.0
+    ptl = np.ascontiguousarray(np.transpose(raw, (1, 0, 2)))
+    co = dict(temperature=B["g3_T"], pressure=B["g3_p"], wavelength=B["g3_lam"])
+    da = {"1H2-16O": DataArrayLike(raw, ("temperature", "pressure", "wavelength"), **co)}
+    _, s_da, T_da, up_da, dn_da = _run(fa, B, da, g="g3")
+    tabs_o = {"1H2-16O": O.Table(ptl, B["g3_p"], B["g3_T"])}
+
+    def run(t=tabs_o):
+        return O.emission_spectrum(t, B["g3_T"], B["g3_p"], B["g3_lam"], O.F_TOA(B["g3_lam"]),
+                                   G_J, M_BAR, 1, n_timesteps=3)
+    osp, oT, _, _, ou, od, _ = run()
+    with perturbed_exp():
+        psp, _, _, _, pu, pd, _ = run()
+    floor = grid_floor(osp, ou, od, psp, pu, pd)
+    assert max(floor) <= 1e-10, floor
+    assert_grid_parity(s_da, osp, up_da, ou, dn_da, od, "groupies strong (10 layers) vs oracle",
+                       T=T_da, ref_T=oT)          # no floor: 1e-10 outright
+    swapped = {"1H2-16O": fa.OpacityTable(np.ascontiguousarray(np.transpose(ptl, (1, 0, 2))),
+                                          B["g3_p"], B["g3_T"])}
+    _, s_sw, _, _, _ = _run(fa, B, swapped, g="g3")
+    assert float(np.max(np.abs(s_sw - osp) / np.abs(osp))) > 1e-4

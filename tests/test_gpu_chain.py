@@ -82,15 +82,20 @@ def test_chained_launches_are_bitwise_identical(fa, nL, q, waves, depth):
             eng.set_option("pipe", 4)
         elif depth:
             eng.set_option("prefetch_depth", depth)
+        launched = {}
         for chain in (2 if q == 1 else 1, 0):   # one-lane and pipe: chained on request
             eng.set_option("chain", chain)
+            n0 = eng.chain_count()
             out[chain] = _exercise(eng, T0, nL, lam.size)
+            launched[chain] = eng.chain_count() - n0
         path = eng.path()
     finally:
         eng.close()
     assert path["contracted"] and (path["paired"], path["quad"]) == (q == 2, q == 4)
     assert (path["pipe"] == 4) == (depth == "pipe")
     on = max(out)
+    # the chain-on runs really chained (else the comparison below is vacuous), the others never
+    assert launched[on] > 0 and launched[0] == 0, launched
     _compare(out[on], out[0], f"Q{q} waves {waves} depth {depth} nL {nL}")
     assert 1 < out[on]["run"]["n_iter"] <= 80
 
@@ -109,6 +114,32 @@ def test_chained_launches_with_p2p_exchange(fa):
             eng.set_option("group_waves", 8)
             eng.set_option("chain", chain)
             out[chain] = _exercise(eng, T0, nL, lam.size)
+            out[chain]["chained"] = eng.chain_count()
         finally:
             eng.close()
+    assert out[1]["chained"] > 0 and out[0]["chained"] == 0
     _compare(out[1], out[0], "p2p")
+
+
+def test_no_chained_launch_while_timing(fa):
+    """Per-sweep HIP events time the sweep alone: with timing on, sweep and update launch
+    separately (a chained launch would also hold the deferred update and its P2P wait)."""
+    nL = 30
+    lam, p, T0, tabs = _case(fa, nL)
+    eng = fa.Engine(lam, p, tabs)
+    try:
+        eng.set_option("group_q", 2)
+        eng.set_option("chain", 1)
+        eng.state_init(T0)
+        eng.iterate(3)
+        eng.synchronize()
+        n0 = eng.chain_count()
+        assert n0 > 0
+        eng.timing(True)
+        eng.iterate(3)
+        eng.synchronize()
+        ms, n = eng.timing_read()
+        eng.timing(False)
+        assert eng.chain_count() == n0 and n == 6 and ms > 0
+    finally:
+        eng.close()

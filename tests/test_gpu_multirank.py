@@ -39,12 +39,13 @@ def _worker(rank, world, port, transport, q):
         out = eng.run(grid.init_temperatures, n_timesteps=60)
         # a second run on the same communicator (sequence numbers continue)
         out2 = eng.run(grid.init_temperatures, n_timesteps=60)
+        chained = eng.chain_count()
         eng.close()
         rdzv.close()
         q.put((rank, lo, hi, out["spectrum"], out["final_T"], out["temp_hist"], out["n_iter"],
-               out2["final_T"], None))
+               out2["final_T"], None, chained))
     except Exception as e:   # reported to the parent, which fails the test
-        q.put((rank, 0, 0, None, None, None, -1, None, repr(e)))
+        q.put((rank, 0, 0, None, None, None, -1, None, repr(e), -1))
 
 
 @pytest.mark.parametrize("transport,world", [("host", 2), ("p2p", 2), ("p2p", 4), ("host", 4),
@@ -64,6 +65,9 @@ def test_ranks_on_one_gpu_match_single_rank(transport, world):
         assert p.exitcode == 0
     for r in res:
         assert r[8] is None, f"rank {r[0]}: {r[8]}"
+        # ranks sharing the GPU never chain launches (the runtime sees the peer mailboxes on its
+        # own device): a chained launch's spinning sweep blocks could starve another rank
+        assert r[9] == 0, f"rank {r[0]}: {r[9]} chained launches on a shared GPU"
     from frei_amd.engine import Engine
     grid, op = _problem()
     eng = Engine(grid.lam, grid.pressures, op, device=0)

@@ -139,3 +139,31 @@ def test_balanced_edges_split_the_measured_cost_evenly():
     assert e[-1] - e[-2] < n // R
     with pytest.raises(ValueError):
         balanced_edges([0, 10, 5], [1.0, 1.0])
+
+
+def test_chemistry_provider_called_on_the_reference_signature():
+    """frei_amd.chemistry.provider_mmr calls a provider as the reference's kappa does
+    (chemistry(T, p, species, m_bar=...), opacity.py:246-248) and reads its dict; the reference's
+    mock as a provider is detected as T-independent, a T-dependent one is not; a species the
+    provider does not return raises."""
+    import numpy as np
+    import importlib
+    C = importlib.import_module("frei_amd.chemistry")   # the package re-exports the function
+    names = ["1H2-16O", "12C-16O"]
+    p = np.array([10.0, 1.0, 0.1])
+    seen = []
+
+    def fake(T, pr, species, return_vmr=False, m_bar=None):
+        seen.append((np.asarray(T).shape, list(species), m_bar))
+        T = np.asarray(getattr(T, "value", T), dtype=float)
+        return {"1H2-16O": 1e-3 * (T / 1000.0), "12C-16O": np.full(T.shape, 2e-3)}
+    v = C.provider_mmr(fake, [1000.0, 2000.0], [1.0, 0.1], names, 4e-24)
+    assert np.allclose(v, [[1e-3, 2e-3], [2e-3, 2e-3]])
+    assert seen[0][1] == names and float(getattr(seen[0][2], "value", seen[0][2])) == 4e-24
+    assert C.fixed_provider_mmr(fake, names, p, 4e-24) is None
+    fixed = C.fixed_provider_mmr(C.chemistry, names, p, 4e-24)
+    mock = C.chemistry(np.full(3, 1000.0), p, names, m_bar=4e-24)
+    assert np.array_equal(fixed, np.array([mock[n] for n in names]))
+    import pytest
+    with pytest.raises(KeyError, match="12C-1H4"):
+        C.provider_mmr(fake, [1000.0], [1.0], names + ["12C-1H4"], 4e-24)

@@ -132,7 +132,7 @@ def main():
     fetch = L.frei_trace_fetch
     fetch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     cap = 1 << 17
-    buf = np.zeros((cap, 6), dtype=np.int64)
+    buf = np.zeros((cap, 8), dtype=np.int64)   # kind, block, 4 wall marks, 2 cycle stamps
     n = ctypes.c_int(0)
     eng.state_init(w["T0"])
     eng.iterate(a.warmup)
