@@ -182,6 +182,8 @@ struct frei_ctx {
   int hist_cap = 0;
   int32_t *d_flips = nullptr, *d_prev = nullptr, *d_ndiff = nullptr;
   int* h_flag = nullptr;  // pinned [2]
+  int* h_err = nullptr;   // pinned [2]: the chained-poll and P2P error flags (check_comm)
+  int64_t chain_checked = 0;   // n_chained at the last check_comm
   hipEvent_t flag_ev[2] = {nullptr, nullptr};
   // comm
   void* comm = nullptr;
@@ -1047,21 +1049,32 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   return 0;
 }
 
-// After a stream synchronize: did a P2P wait time out (a rank never published its sums)?
+// After a stream synchronize: did a chained sweep's poll or a P2P wait time out (a rank never
+// published its sums)?  The flags are read only when they can have been set — a chained launch
+// since the last check, a P2P communicator — and into pinned memory on the context's stream: a
+// pageable hipMemcpy here cost ~20 ms the first time (its staging buffer), which left the GPU
+// idle right before a timed loop (bench.py's warm-up synchronize) and changed how the power
+// management clocked the loop that followed (profiles/r04/bisect/README.md).
 int check_comm(frei_ctx* c) {
-  if (c->d_chain_err) {
-    int e = 0;
-    HIP_TRY(hipMemcpy(&e, c->d_chain_err, sizeof(int), hipMemcpyDeviceToHost));
-    if (e) {   // reported once: rearm it so later runs on this context are not failed by it
-      c->has_pend = false;
-      HIP_TRY(hipMemset(c->d_chain_err, 0, sizeof(int)));
-      return fail("chained sweep: the update workgroups never published the temperatures");
-    }
+  const bool chain = c->d_chain_err && c->n_chained != c->chain_checked;
+  const bool comm = c->d_comm_err != nullptr;
+  if (!chain && !comm) return 0;
+  if (chain)
+    HIP_TRY(hipMemcpyAsync(&c->h_err[0], c->d_chain_err, sizeof(int), hipMemcpyDeviceToHost,
+                           c->stream));
+  if (comm)
+    HIP_TRY(hipMemcpyAsync(&c->h_err[1], c->d_comm_err, sizeof(int), hipMemcpyDeviceToHost,
+                           c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->chain_checked = c->n_chained;
+  if (chain && c->h_err[0]) {   // reported once: rearm it so later runs are not failed by it
+    c->has_pend = false;
+    c->h_err[0] = 0;
+    HIP_TRY(hipMemsetAsync(c->d_chain_err, 0, sizeof(int), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return fail("chained sweep: the update workgroups never published the temperatures");
   }
-  if (!c->d_comm_err) return 0;
-  int e = 0;
-  HIP_TRY(hipMemcpy(&e, c->d_comm_err, sizeof(int), hipMemcpyDeviceToHost));
-  if (e)
+  if (comm && c->h_err[1])
     return fail("P2P exchange timed out: a peer rank did not publish its partial sums "
                 "(FREI_P2P_TIMEOUT_S)");
   return 0;
@@ -1142,8 +1155,10 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
       (rc = dalloc(&c->d_ndiff, NL * A)) || (A > 1 && (rc = dalloc(&c->d_g, A))))
     return bail(rc);
   c->d_T_home = c->d_T;
-  if (hipHostMalloc((void**)&c->h_flag, 2 * sizeof(int)) != hipSuccess)
+  if (hipHostMalloc((void**)&c->h_flag, 2 * sizeof(int)) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_err, 2 * sizeof(int)) != hipSuccess)
     return bail(fail("hipHostMalloc failed"));
+  c->h_err[0] = c->h_err[1] = 0;
   for (int k = 0; k < 2; ++k)
     if (hipEventCreateWithFlags(&c->flag_ev[k], hipEventDisableTiming) != hipSuccess)
       return bail(fail("hipEventCreate failed"));
@@ -1209,6 +1224,7 @@ int frei_ctx_destroy(frei_ctx* c) {
   for (void* p : vv)
     if (p) (void)hipFree(p);
   if (c->h_flag) (void)hipHostFree(c->h_flag);
+  if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_conv) (void)hipHostFree(c->h_conv);
   dfree(c->d_g);
   if (c->h_ag) (void)hipHostFree(c->h_ag);

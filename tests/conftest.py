@@ -13,9 +13,37 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: multi-second CPU test")
 
 
+_OUTCOMES = {"passed": 0, "failed": 0, "skipped": 0}
+
+
+def pytest_runtest_logreport(report):
+    if report.when == "call" or (report.when == "setup" and report.outcome != "passed"):
+        _OUTCOMES[report.outcome] = _OUTCOMES.get(report.outcome, 0) + 1
+
+
+def _provenance(session, exitstatus):
+    """Which tree and run produced a parity log: the git head recorded in .tree_stamp
+    (tools/stamp_tree.sh writes it before a GPU call: the box's snapshot has no .git), the
+    source hash the native library was built from, host, time, the pytest arguments and the
+    session's outcome counts."""
+    import datetime
+    import socket
+    prov = {"host": socket.gethostname(),
+            "utc": datetime.datetime.now(datetime.timezone.utc).isoformat(timespec="seconds"),
+            "pytest_args": [str(a) for a in session.config.invocation_params.args],
+            "exitstatus": int(exitstatus), "outcomes": dict(_OUTCOMES)}
+    for key, name in (("tree", ".tree_stamp"), ("lib_source_hash", "frei_amd/libfrei_hip.so.stamp")):
+        try:
+            with open(os.path.join(ROOT, name)) as f:
+                prov[key] = f.read().strip()
+        except OSError:
+            prov[key] = None
+    return prov
+
+
 def pytest_sessionfinish(session, exitstatus):
     """With FREI_PARITY_JSON set, write the observed grid-level parity errors of the session
-    (tests/parity.py PARITY_LOG) there."""
+    (tests/parity.py PARITY_LOG) there, with the provenance of the run."""
     path = os.environ.get("FREI_PARITY_JSON")
     if not path:
         return
@@ -28,7 +56,8 @@ def pytest_sessionfinish(session, exitstatus):
              for k in ("spectrum_elementwise", "F_up_rownorm", "F_down_rownorm",
                        "T_elementwise")}
     with open(path, "w") as f:
-        json.dump({"criterion": "tests/parity.py assert_grid_parity: spectrum elementwise, "
+        json.dump({"provenance": _provenance(session, exitstatus),
+                   "criterion": "tests/parity.py assert_grid_parity: spectrum elementwise, "
                                 "F_up/F_down row-normwise <= max(1e-10, 2 x one-ulp floor); "
                                 "T elementwise <= 1e-10",
                    "entries": PARITY_LOG, "worst": worst,
