@@ -6,6 +6,13 @@
 #include <cstdint>
 #include <string>
 
+// The sweeps' coefficient form (frei_kernels.hip StepCoef): 1 = premultiplied by 1/chi with pi
+// in the Planck prefactor (the runtime hands the fast sweeps pi 2hc^2/lam^5), 0 = the
+// reference's literal expression order.
+#ifndef FREI_LEAN
+#define FREI_LEAN 1
+#endif
+
 namespace frei {
 
 // CODATA 2018 (astropy 4.3.1, the reference's unit backend), cgs.

@@ -448,17 +448,49 @@ __device__ __forceinline__ int64_t uni(int64_t x) {
 #define UNIV(x) uni(x)
 #endif
 
+// FREI_LEAN (default 1): the step's coefficients premultiplied by 1/chi and the source terms
+// formed with the identities of twostream.py:143-176 — zm^2 - zp^2 = -r, (xi + psi) - chi =
+// -((chi - psi) - xi) — and pi folded into the Planck prefactor (FastArgs.c1 = pi 2hc^2/lam^5),
+// so a flux update is two fma on the carried input: 12 VALU fewer per update than the
+// reference's literal expression order (0), equal to it within a few ulps.
+// Every sweep form (one-lane, grouped-lane, producer/consumer) uses the same coefficients, so
+// they stay bitwise identical to each other.
 struct StepCoef {
-  double psi, xi, ic, Xu, Xd;  // F2u = ic*((psi*F1u - xi*F2d) + Xu), F1d likewise with Xd
+  // FREI_LEAN 0: F2u = ic*((psi*F1u - xi*F2d) + Xu), F1d = ic*((psi*F2d - xi*F1u) + Xd)
+  // FREI_LEAN 1: psi, xi, Xu, Xd hold ic*psi, ic*xi, ic*Xu, ic*Xd (ic unused):
+  //              F2u = psi F1u - xi F2d + Xu, F1d = psi F2d - xi F1u + Xd (step_up / step_dn)
+  double psi, xi, ic, Xu, Xd;
   double dtau, Bnext;          // Bnext: Planck value the next layer reuses
   double F_st;                 // stale opposite-stream flux
   int layer, top;
 };
 
+// The flux update of one step from its coefficients (twostream.py:161-176).
+__device__ __forceinline__ double step_up(double psi, double xi, double ic, double Xu,
+                                          double F1u, double F2d) {
+#if FREI_LEAN
+  (void)ic;
+  return __builtin_fma(psi, F1u, __builtin_fma(-xi, F2d, Xu));
+#else
+  return ic * ((psi * F1u - xi * F2d) + Xu);
+#endif
+}
+__device__ __forceinline__ double step_dn(double psi, double xi, double ic, double Xd,
+                                          double F1u, double F2d) {
+#if FREI_LEAN
+  (void)ic;
+  return __builtin_fma(psi, F2d, __builtin_fma(-xi, F1u, Xd));
+#else
+  return ic * ((psi * F2d - xi * F1u) + Xd);
+#endif
+}
+
 // Terms after E (twostream.py:143-176), same expression order as two_stream().  pi_w =
 // pi (1 - w0) / (E - w0) comes from the caller; 1 / chi is formed within an ulp (it scales
 // the whole update, nothing cancels after it); the transmission's exp argument is <= 0.
 // NF: the step's inputs cannot be NaN (contracted-table sweeps), so exp's clamp is a max.
+// FREI_LEAN: B1, B2 and q carry the factor pi (c1 = pi 2hc^2/lam^5) and pi_w is the remaining
+// (1 - w0) / (E - w0) (exactly 1 where E = 1); the coefficients come out premultiplied by 1/chi.
 template <bool NF = false>
 __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, double B2,
                                           double sq, double r, double q, double pi_w,
@@ -470,6 +502,21 @@ __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, dou
   const double Tr2 = Tr * Tr;
   const double zm2 = zm * zm;
   const double zp2 = zp * zp;
+#if FREI_LEAN
+  const double chi = __builtin_fma(zm2, Tr2, -zp2);
+  const double xi = (zp * zm) * (1.0 - Tr2);
+  const double psi = -(r * Tr);                      // (zm^2 - zp^2) Tr
+  const double ic = fm::rcp_nr(chi);
+  const double u = chi + xi;
+  const double v = (chi - psi) - xi;                 // -((xi + psi) - chi)
+  const double qv = q * v;
+  const double icw = ic * pi_w;
+  c.psi = ic * psi;
+  c.xi = ic * xi;
+  c.ic = 1.0;
+  c.Xu = icw * ((B2 * u - psi * B1) + qv);
+  c.Xd = icw * ((B1 * u - psi * B2) - qv);
+#else
   const double chi = zm2 * Tr2 - zp2;
   const double xi = (zp * zm) * (1.0 - Tr2);
   const double psi = (zm2 - zp2) * Tr;
@@ -478,6 +525,7 @@ __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, dou
   c.ic = fm::rcp_nr(chi);
   c.Xu = pi_w * ((B2 * (chi + xi) - psi * B1) + q * ((chi - psi) - xi));
   c.Xd = pi_w * ((B1 * (chi + xi) - psi * B2) + q * ((xi + psi) - chi));
+#endif
   c.dtau = dtau;
 }
 
@@ -489,7 +537,9 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
   const double Emw = E - w0;
   const double q = fm::div(fm::div(B1 - B2, dtau), 2.0 * E);
   // E = 1 lanes take pi like coef_e1, so both forms give the same bits on them
-#if FREI_PI_E1
+#if FREI_LEAN
+  const double pi_w = (w0 > 0.1) ? fm::div(1.0 - w0, Emw) : 1.0;   // pi is in B1, B2
+#elif FREI_PI_E1
   const double pi_w = (w0 > 0.1) ? fm::div(kPi * (1.0 - w0), Emw) : kPi;
 #else
   const double pi_w = fm::div(kPi * (1.0 - w0), Emw);
@@ -508,7 +558,9 @@ __device__ __forceinline__ void coef_e1(double w0, double dtau, double B1, doubl
                                         StepCoef& c) {
   const double Emw = 1.0 - w0;
   const double sq = fm::sqrt_pos(Emw);
-#if FREI_PI_E1
+#if FREI_LEAN
+  coef_tail<NF>(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5, 1.0, c);
+#elif FREI_PI_E1
   coef_tail<NF>(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5, kPi, c);
 #else
   coef_tail<NF>(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5,
@@ -835,8 +887,8 @@ __device__ __forceinline__ void sweep_fast_body(
   auto finish = [&](int k, const StepCoef& c, double F_st) {
     double F1u, F2d;
     if (DIR == kEmit) { F1u = carry; F2d = F_st; } else { F2d = carry; F1u = F_st; }
-    const double F2u = c.ic * ((c.psi * F1u - c.xi * F2d) + c.Xu);
-    const double F1d = c.ic * ((c.psi * F2d - c.xi * F1u) + c.Xd);
+    const double F2u = step_up(c.psi, c.xi, c.ic, c.Xu, F1u, F2d);
+    const double F1d = step_dn(c.psi, c.xi, c.ic, c.Xd, F1u, F2d);
     if (k >= ns) return;
     const int i = c.layer;
     if (act) {
@@ -1143,11 +1195,11 @@ __device__ __forceinline__ void sweep_group_body(
     // the two fluxes of a step from its carried input (same expressions as the one-lane form)
     auto flux_up = [&](double in) {   // F_2_up
       const double F1u = (DIR == kEmit) ? in : F_st, F2d = (DIR == kEmit) ? F_st : in;
-      return c.ic * ((c.psi * F1u - c.xi * F2d) + c.Xu);
+      return step_up(c.psi, c.xi, c.ic, c.Xu, F1u, F2d);
     };
     auto flux_dn = [&](double in) {   // F_1_down
       const double F1u = (DIR == kEmit) ? in : F_st, F2d = (DIR == kEmit) ? F_st : in;
-      return c.ic * ((c.psi * F2d - c.xi * F1u) + c.Xd);
+      return step_dn(c.psi, c.xi, c.ic, c.Xd, F1u, F2d);
     };
     // the carried chain runs through the group's steps in order, each step in its own lane
     // (q == r); only the carried flux is formed in the chain, the other one once afterwards
@@ -1333,7 +1385,7 @@ void launch_sweep_group(int dir, int Q, int NW, const FastArgs& a, int nblocks,
 //   phase ph: producer p computes the coefficients of the M consecutive steps
 //             ph G + p M ... (+ M - 1), G = 3 M, with the one-lane form's arithmetic (Planck
 //             reused inside its M steps, formed afresh at the first) into an LDS ring slot
-//             [ph & 1][G steps][psi, xi, ic, Xu, Xd][64 lanes] and writes dtau;
+//             [ph & 1][G steps][psi, xi, Xu, Xd (, ic)][64 lanes] and writes dtau;
 //             the consumer runs the carried chain over phase ph - 1's G steps from the other
 //             slot (stale fluxes prefetched a phase ahead), stores the fluxes and stages the
 //             bolometric terms exactly as the one-lane sweep does;
@@ -1346,7 +1398,7 @@ void launch_sweep_group(int dir, int Q, int NW, const FastArgs& a, int nblocks,
 // for bit.  One contracted table (K3, mmr = 1); the step records come from the global step table
 // through scalar loads.
 constexpr int kPipeP = 3;    // producer waves per consumer wave
-constexpr int kPipeNV = 5;   // psi, xi, ic, Xu, Xd
+constexpr int kPipeNV = FREI_LEAN ? 4 : 5;   // psi, xi, Xu, Xd (+ ic: FREI_LEAN 0)
 constexpr int kStepDoubles = (int)(sizeof(FastStepS) / sizeof(double));
 __host__ __device__ inline int64_t pipe_lds_doubles(int NC, int M, int ns) {
   return (int64_t)NC * 2 * (kPipeP * M) * kPipeNV * 64 + (int64_t)NC * 2 * 4 * kStageRow +
@@ -1509,9 +1561,9 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
         const int s = p * M + i;
         *rslot(ph, s, 0) = c[i].psi;
         *rslot(ph, s, 1) = c[i].xi;
-        *rslot(ph, s, 2) = c[i].ic;
-        *rslot(ph, s, 3) = c[i].Xu;
-        *rslot(ph, s, 4) = c[i].Xd;
+        *rslot(ph, s, 2) = c[i].Xu;
+        *rslot(ph, s, 3) = c[i].Xd;
+        if constexpr (kPipeNV == 5) *rslot(ph, s, kPipeNV - 1) = c[i].ic;
         if (dtaus && act && kb + i < ns) dtaus[(int64_t)(kb + i + 1) * nl + j] = c[i].dtau;
       }
     };
@@ -1554,15 +1606,15 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
     double* t0 = tile + (int64_t)sub * 2 * 4 * kStageRow;
     // step i of phase q: the carried chain, flux stores and staged bolometric terms (a pair's
     // 8 sums after its second step)
-    // (rv: the step's psi, xi, ic, Xu, Xd, read from the ring with the rest of its phase's)
+    // (rv: the step's psi, xi, Xu, Xd (, ic), read from the ring with the rest of its phase's)
     auto step = [&](int q, int i, double stv, const double (&rv)[kPipeNV]) {
       const int k = q * G + i;
       if (k < ns) {
-        const double psi = rv[0], xi = rv[1], ic = rv[2], Xu = rv[3], Xd = rv[4];
+        const double psi = rv[0], xi = rv[1], Xu = rv[2], Xd = rv[3], ic = rv[kPipeNV - 1];
         double F1u, F2d;
         if (DIR == kEmit) { F1u = carry; F2d = stv; } else { F2d = carry; F1u = stv; }
-        const double F2u = ic * ((psi * F1u - xi * F2d) + Xu);
-        const double F1d = ic * ((psi * F2d - xi * F1u) + Xd);
+        const double F2u = step_up(psi, xi, ic, Xu, F1u, F2d);
+        const double F1d = step_dn(psi, xi, ic, Xd, F1u, F2d);
         const int layer = step_layer(DIR, k, nL);
         const bool top = DIR == kEmit && k == ns - 1;
 #ifndef FREI_PIPE_NOSTORE   // diagnostic ablation build: no flux stores

@@ -63,17 +63,20 @@ def test_batched_atmospheres_match_oracle_per_atmosphere(fa, monkeypatch, k7_mfm
             tabs_o, T0[m], p, lam, Ft, g[m], M_BAR, 1, n_timesteps=40, n_zero_crossings=2,
             convergence_dT=3.0, mmr=mmr[m], err=cond)
         assert out["n_iter"][m] == it, f"atmosphere {m}: iterations"
-        relT = rel(out["final_T"][m], oT)
-        assert relT < 1e-10, f"atmosphere {m}: T {relT:.3e}"
-        assert_flux_parity(out["spectra"][m], osp, cond["up"][-1], max(EPS, relT),
-                           f"atmosphere {m} spectrum")
         with perturbed_exp():
-            psp, _, _, _, pu, pd, _ = O.emission_spectrum(
+            psp, pT, _, _, pu, pd, _ = O.emission_spectrum(
                 tabs_o, T0[m], p, lam, Ft, g[m], M_BAR, 1, n_timesteps=40, n_zero_crossings=2,
                 convergence_dT=3.0, mmr=mmr[m])
+        # 40 iterations without meeting the convergence test: one ulp of exp moves the oracle's
+        # own T by up to 1.1e-10 here (atmosphere 3), so T is held to 1e-10 or twice that floor
+        T_floor = rel(pT, oT)
+        relT = rel(out["final_T"][m], oT)
+        assert relT <= max(1e-10, 2 * T_floor), f"atmosphere {m}: T {relT:.3e} (floor {T_floor:.3e})"
+        assert_flux_parity(out["spectra"][m], osp, cond["up"][-1], max(EPS, relT),
+                           f"atmosphere {m} spectrum")
         floor = grid_floor(osp, ou, od, psp, pu, pd)
         assert_grid_parity(out["spectra"][m], osp, ups[m], ou, downs[m], od, f"atmosphere {m}",
-                           floor, T=out["final_T"][m], ref_T=oT)
+                           floor, T=out["final_T"][m], ref_T=oT, T_floor=T_floor)
 
 
 @pytest.mark.parametrize("k7_mfma", ["1", "0"])
