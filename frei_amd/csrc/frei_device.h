@@ -6,9 +6,8 @@
 #include <cstdint>
 #include <string>
 
-// The sweeps' coefficient form (frei_kernels.hip StepCoef): 1 = premultiplied by 1/chi with pi
-// in the Planck prefactor (the runtime hands the fast sweeps pi 2hc^2/lam^5), 0 = the
-// reference's literal expression order.
+// The sweeps' coefficient form (frei_kernels.hip StepCoef): 1 = premultiplied by 1/chi and
+// pi_w (two fma per flux update), 0 = the reference's literal association.
 #ifndef FREI_LEAN
 #define FREI_LEAN 1
 #endif

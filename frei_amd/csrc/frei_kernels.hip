@@ -448,13 +448,12 @@ __device__ __forceinline__ int64_t uni(int64_t x) {
 #define UNIV(x) uni(x)
 #endif
 
-// FREI_LEAN (default 1): the step's coefficients premultiplied by 1/chi and the source terms
-// formed with the identities of twostream.py:143-176 — zm^2 - zp^2 = -r, (xi + psi) - chi =
-// -((chi - psi) - xi) — and pi folded into the Planck prefactor (FastArgs.c1 = pi 2hc^2/lam^5),
-// so a flux update is two fma on the carried input: 12 VALU fewer per update than the
-// reference's literal expression order (0), equal to it within a few ulps.
-// Every sweep form (one-lane, grouped-lane, producer/consumer) uses the same coefficients, so
-// they stay bitwise identical to each other.
+// FREI_LEAN (default 1): the step's coefficients premultiplied by 1/chi (and pi_w), so a flux
+// update is two fma on the carried input, F2u = (ic psi) F1u - (ic xi) F2d + (ic pi_w) Xu,
+// instead of ic ((psi F1u - xi F2d) + pi_w Xu): a different association of the same products
+// (an ulp or so, tools/lean_err.py), fewer instructions on the carried chain and four ring
+// values per step in the producer/consumer sweep instead of five.  Every sweep form uses the
+// same coefficients, so they stay bitwise identical to each other.
 struct StepCoef {
   // FREI_LEAN 0: F2u = ic*((psi*F1u - xi*F2d) + Xu), F1d = ic*((psi*F2d - xi*F1u) + Xd)
   // FREI_LEAN 1: psi, xi, Xu, Xd hold ic*psi, ic*xi, ic*Xu, ic*Xd (ic unused):
@@ -503,19 +502,21 @@ __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, dou
   const double zm2 = zm * zm;
   const double zp2 = zp * zp;
 #if FREI_LEAN
-  const double chi = __builtin_fma(zm2, Tr2, -zp2);
+  // chi, xi, psi and the source brackets exactly as the reference forms them: their rounding
+  // errors are correlated ((chi - psi) - xi cancels to O(dtau^2) in thin layers), so rewriting
+  // any of them by an algebraic identity (psi = -r Tr, an fma for chi, (xi + psi) - chi as
+  // -((chi - psi) - xi)) moved thin-layer fluxes by up to 1e-8 (tools/lean_err.py)
+  const double chi = zm2 * Tr2 - zp2;
   const double xi = (zp * zm) * (1.0 - Tr2);
-  const double psi = -(r * Tr);                      // (zm^2 - zp^2) Tr
+  const double psi = (zm2 - zp2) * Tr;
   const double ic = fm::rcp_nr(chi);
   const double u = chi + xi;
-  const double v = (chi - psi) - xi;                 // -((xi + psi) - chi)
-  const double qv = q * v;
   const double icw = ic * pi_w;
   c.psi = ic * psi;
   c.xi = ic * xi;
   c.ic = 1.0;
-  c.Xu = icw * ((B2 * u - psi * B1) + qv);
-  c.Xd = icw * ((B1 * u - psi * B2) - qv);
+  c.Xu = icw * ((B2 * u - psi * B1) + q * ((chi - psi) - xi));
+  c.Xd = icw * ((B1 * u - psi * B2) + q * ((xi + psi) - chi));
 #else
   const double chi = zm2 * Tr2 - zp2;
   const double xi = (zp * zm) * (1.0 - Tr2);
@@ -537,9 +538,7 @@ __device__ __forceinline__ void coef_from(double w0, double dtau, double B1, dou
   const double Emw = E - w0;
   const double q = fm::div(fm::div(B1 - B2, dtau), 2.0 * E);
   // E = 1 lanes take pi like coef_e1, so both forms give the same bits on them
-#if FREI_LEAN
-  const double pi_w = (w0 > 0.1) ? fm::div(1.0 - w0, Emw) : 1.0;   // pi is in B1, B2
-#elif FREI_PI_E1
+#if FREI_PI_E1 || FREI_LEAN
   const double pi_w = (w0 > 0.1) ? fm::div(kPi * (1.0 - w0), Emw) : kPi;
 #else
   const double pi_w = fm::div(kPi * (1.0 - w0), Emw);
@@ -558,9 +557,7 @@ __device__ __forceinline__ void coef_e1(double w0, double dtau, double B1, doubl
                                         StepCoef& c) {
   const double Emw = 1.0 - w0;
   const double sq = fm::sqrt_pos(Emw);
-#if FREI_LEAN
-  coef_tail<NF>(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5, 1.0, c);
-#elif FREI_PI_E1
+#if FREI_PI_E1 || FREI_LEAN
   coef_tail<NF>(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5, kPi, c);
 #else
   coef_tail<NF>(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5,

@@ -101,7 +101,6 @@ struct frei_ctx {
   int64_t nlam = 0;
   int nblocks = 0;
   // grid
-  double* d_c1pi = nullptr;              // pi 2hc^2/lam^5: the fast sweeps' Planck prefactor (FREI_LEAN)
   double *d_c1 = nullptr, *d_hcl = nullptr, *d_sig = nullptr, *d_ftoa = nullptr,
          *d_wtr = nullptr, *d_p = nullptr, *d_lnp = nullptr;
   std::vector<double> p;
@@ -752,7 +751,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
     f.n_steps = ns;
     f.force = o.force;
     f.live_only = o.live_only;
-    f.c1 = FREI_LEAN ? c->d_c1pi : c->d_c1;   // pi folded into the Planck prefactor
+    f.c1 = c->d_c1;
     f.hcl = c->d_hcl;
     f.sig = c->d_sig;
     f.wtr = c->d_wtr;
@@ -1137,7 +1136,7 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
     return bail(fail("hipStreamCreate failed"));
   const size_t NL = n_layers, NS = n_species, ns = n_layers - 1, A = n_atm;
   const size_t F = NL * (size_t)n_lam * A;   // per-atmosphere buffers are n_atm blocks
-  if ((rc = dalloc(&c->d_c1, n_lam)) || (rc = dalloc(&c->d_c1pi, n_lam)) || (rc = dalloc(&c->d_hcl, n_lam)) ||
+  if ((rc = dalloc(&c->d_c1, n_lam)) || (rc = dalloc(&c->d_hcl, n_lam)) ||
       (rc = dalloc(&c->d_sig, n_lam)) || (rc = dalloc(&c->d_ftoa, n_lam)) ||
       (rc = dalloc(&c->d_wtr, n_lam)) || (rc = dalloc(&c->d_p, NL)) || (rc = dalloc(&c->d_lnp, NL)) ||
       (rc = dalloc(&c->d_Fu, F)) || (rc = dalloc(&c->d_Fd, F)) ||
@@ -1214,7 +1213,7 @@ int frei_ctx_destroy(frei_ctx* c) {
   dfree(c->d_chem_pj);
   dfree(c->d_ones);
   dfree(c->d_prow);
-  double* dd[] = {c->d_c1, c->d_c1pi, c->d_hcl, c->d_sig, c->d_ftoa, c->d_wtr, c->d_p, c->d_lnp,
+  double* dd[] = {c->d_c1, c->d_hcl, c->d_sig, c->d_ftoa, c->d_wtr, c->d_p, c->d_lnp,
                   c->d_Fu, c->d_Fd, c->d_T, c->d_T_alt, c->d_T3, c->d_dT, c->d_dtaus, c->d_bol, c->d_tnodes, c->d_mmr, c->d_part,
                   c->d_Fb, c->d_Fb_all, c->d_Tb, c->d_Ta, c->d_hist};
   for (double* p : dd)
@@ -1257,11 +1256,6 @@ int frei_set_grid(frei_ctx* c, const double* c1, const double* lk, const double*
     TRY(h2d(c->d_g, gv.data(), gv.size(), c->stream));
   }
   TRY(h2d(c->d_c1, c1, n, c->stream));
-  {
-    std::vector<double> c1pi(c1, c1 + n);
-    for (double& x : c1pi) x *= kPi;
-    TRY(h2d(c->d_c1pi, c1pi.data(), n, c->stream));
-  }
   {   // the Planck exponent's per-wavelength factor hc / (lam k_B) (kernels: times 1 / T)
     std::vector<double> hcl(n);
     for (int64_t j = 0; j < n; ++j) hcl[j] = kHC / lk[j];
