@@ -418,6 +418,44 @@ __device__ __forceinline__ void ring_fence() {
   __builtin_amdgcn_sched_barrier(0);
 #endif
 }
+// A register-level dependence of a refill's address on the value that consumed the slot (no
+// instruction): sched_barrier only orders the machine scheduler, while instruction selection had
+// already placed the refill loads ahead of the opacity that reads the slot, so the old and new
+// values overlapped and the loop latch copied the four row registers after waiting for their
+// loads (s_waitcnt vmcnt(5..2) + five v_mov_b64 per two steps).  FREI_RING_DEP=0: off (A/B).
+#ifndef FREI_RING_DEP
+#define FREI_RING_DEP 1
+#endif
+// (On the element index, not the pointer: a pointer out of an asm is generic, and its loads
+// would become flat loads that also wait on the LDS counter.)
+template <class I>
+__device__ __forceinline__ I after_use(I idx, double used) {
+#if FREI_RING_DEP
+  asm volatile("" : "+v"(idx) : "v"(used));
+#else
+  (void)used;
+#endif
+  return idx;
+}
+template <class I>
+__device__ __forceinline__ I after_use(I idx, double used, double used2) {
+#if FREI_RING_DEP
+  asm volatile("" : "+v"(idx) : "v"(used), "v"(used2));
+#else
+  (void)used;
+  (void)used2;
+#endif
+  return idx;
+}
+// A value read on every path (no instruction): a load left pending on a rarely taken path makes
+// the loop's merge blocks wait for everything issued after it (vmcnt is in order).
+__device__ __forceinline__ void consume(double v) {
+#if FREI_RING_DEP
+  asm volatile("" ::"v"(v));
+#else
+  (void)v;
+#endif
+}
 
 // Carry-independent part of one step (everything in twostream.py:135-176 except the
 // terms that multiply the carried flux).  Split out so two layers' coefficients form one
@@ -752,7 +790,7 @@ __device__ __forceinline__ void sweep_fast_body(
   // Loads of a step: the 2S table rows (with shared brackets the row offset comes from the
   // step table) and the stale opposite-stream flux.  Unconditional, at clamped indices, so the
   // vmcnt bookkeeping stays static.
-  auto load_rows = [&](int k, double (&v)[2 * S]) {
+  auto load_rows = [&](int k, double (&v)[2 * S], double dep = 0.0) {
     k = k < ns ? k : ns - 1;
 #ifdef FREI_CACHEONLY   // diagnostic build: same instructions, loads from a cache-resident 32 KB
     {
@@ -769,7 +807,7 @@ __device__ __forceinline__ void sweep_fast_body(
       const int64_t off = uni(sp[k].off);
 #pragma unroll
       for (int s = 0; s < S; ++s) {
-        const double* r = a.tab[s] + off + j;
+        const double* r = a.tab[s] + after_use(off + j, dep);
         v[2 * s] = stream_load(r);
         v[2 * s + 1] = stream_load(r + a.pitch);
       }
@@ -777,7 +815,7 @@ __device__ __forceinline__ void sweep_fast_body(
     }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const double* r = a.tab[s] + st[k].off[s] + j;
+      const double* r = a.tab[s] + after_use(st[k].off[s] + j, dep);
       v[2 * s] = stream_load(r);
       v[2 * s + 1] = stream_load(r + a.pitch);
     }
@@ -819,33 +857,31 @@ __device__ __forceinline__ void sweep_fast_body(
   // Phase A of step k from its opacity: dtau, single-scattering albedo and the Planck terms,
   // everything before E.
   // Bprev: emit -> B(T1) of this step, absorb -> B(T2) of this step (reuse, Q: B2 = next B1).
-  auto coef = [&](int k, double tot, double Bprev, StepCoef& c, PreCoef& pc) {
+  // The step's new Planck value (emit: B(T2), absorb: B(T1)); formed ahead of the opacity so the
+  // loop consumes (and refills) its row slots after both steps' Planck chains.
+  auto planck_new = [&](int k) {
     const int kk = k < ns ? k : ns - 1;
-    double iT1, iT2, dm;   // inverse temperatures of the step's layers
-    if constexpr (SH) {
-      c.layer = layer_of(kk);
-      c.top = top_of(kk);
-      iT1 = UNIV(sp[kk].iT1);
-      iT2 = UNIV(sp[kk].iT2);
-      dm = UNIV(sp[kk].dm);
-    } else {
-      c.layer = layer_of(kk);
-      c.top = top_of(kk);
-      iT1 = st[kk].iT1;
-      iT2 = st[kk].iT2;
-      dm = st[kk].dm;
-    }
+    if constexpr (SH) return planck(c1, hcl, DIR == kEmit ? UNIV(sp[kk].iT2) : UNIV(sp[kk].iT1), ek);
+    else return planck(c1, hcl, DIR == kEmit ? st[kk].iT2 : st[kk].iT1, ek);
+  };
+  auto coef = [&](int k, double tot, double Bprev, double X, StepCoef& c, PreCoef& pc) {
+    const int kk = k < ns ? k : ns - 1;
+    double dm;
+    c.layer = layer_of(kk);
+    c.top = top_of(kk);
+    if constexpr (SH) dm = UNIV(sp[kk].dm);
+    else dm = st[kk].dm;
     const double kap = tot + sig;
     const double dtau = dm * kap;
     const double w0 = fm::div(sig, sig + kap);
     double B1, B2;
     if (DIR == kEmit) {
       B1 = Bprev;
-      B2 = c.top ? Bprev : planck(c1, hcl, iT2, ek);
+      B2 = c.top ? Bprev : X;
       c.Bnext = B2;
     } else {
       B2 = Bprev;
-      B1 = planck(c1, hcl, iT1, ek);
+      B1 = X;
       c.Bnext = B1;
     }
     pc.w0 = w0;
@@ -867,6 +903,9 @@ __device__ __forceinline__ void sweep_fast_body(
     bool e1 = true;
 #pragma unroll
     for (int b = 0; b < PD; ++b) e1 = e1 && !(pc[b].w0 > 0.1);
+#ifdef FREI_ISA_E1ONLY   // ISA-histogram build (tools/isa_hist.py): the E = 1 path alone
+    e1 = true;
+#endif
     if (__all(e1)) {
 #pragma unroll
       for (int b = 0; b < PD; ++b)
@@ -882,6 +921,9 @@ __device__ __forceinline__ void sweep_fast_body(
   // Carry-dependent finish of step k: fluxes, stores, bolometric partials.
   double carry;
   auto finish = [&](int k, const StepCoef& c, double F_st) {
+    // read the stale flux on every path, the dummy step past the end included: left pending
+    // there, its load made the loop's merge block wait for the next rows before the refill
+    consume(F_st);
     double F1u, F2d;
     if (DIR == kEmit) { F1u = carry; F2d = F_st; } else { F2d = carry; F1u = F_st; }
     const double F2u = step_up(c.psi, c.xi, c.ic, c.Xu, F1u, F2d);
@@ -941,11 +983,15 @@ __device__ __forceinline__ void sweep_fast_body(
   // loop's back edge, with no copy there (a copy of a register whose load is in flight would
   // make the compiler drain every outstanding load at the latch, vmcnt(0)).
   double vb[PF][2 * S], sb[PF];
+  // rows first, then the stale fluxes: the order the loop refills them in, so the first trip's
+  // waits on its rows are the loop's own (vmcnt is in order: a stale load issued between two
+  // row loads would have to land before the opacity could read the later row)
 #pragma unroll
-  for (int b = 0; b < PF; ++b) {
-    load_rows(b, vb[b]);
-    load_stale(b, sb[b]);
-  }
+  for (int b = 0; b < PF; ++b) load_rows(b, vb[b]);
+  ring_fence();
+#pragma unroll
+  for (int b = 0; b < PF; ++b) load_stale(b, sb[b]);
+  ring_fence();
   for (int k0 = 0; k0 < ns; k0 += PF) {
 #pragma unroll
   for (int g = 0; g < PF / PD; ++g) {
@@ -953,16 +999,18 @@ __device__ __forceinline__ void sweep_fast_body(
     if (PF > PD && k >= ns) break;   // wave-uniform: no dummy coefficient blocks at the end
     StepCoef c[PD];
     PreCoef pc[PD];
-    double tot[PD];
+    double tot[PD], X[PD];
+#pragma unroll
+    for (int b = 0; b < PD; ++b) X[b] = planck_new(k + b);
 #pragma unroll
     for (int b = 0; b < PD; ++b) tot[b] = opacity(k + b, vb[g * PD + b]);
     ring_fence();
 #pragma unroll
-    for (int b = 0; b < PD; ++b) load_rows(k + b + PF, vb[g * PD + b]);
+    for (int b = 0; b < PD; ++b) load_rows(k + b + PF, vb[g * PD + b], tot[b]);
     double Bp = Bc;
 #pragma unroll
     for (int b = 0; b < PD; ++b) {
-      coef(k + b, tot[b], Bp, c[b], pc[b]);
+      coef(k + b, tot[b], Bp, X[b], c[b], pc[b]);
       Bp = c[b].Bnext;
     }
     Bc = Bp;
@@ -1115,8 +1163,10 @@ __device__ __forceinline__ void sweep_group_body(
   // across its refill and the loop's back edge needs no register copies (a copy of an
   // in-flight load drains every outstanding load there).
   int kr = q, kst = q;               // this lane's step of the next row / stale load
-  auto load_rows = [&](Pre& P) {
-    const FastStepS& st = sp[clampk(kr)];
+  // d1, d2: values formed from the buffer's previous contents (after_use: the refill is issued
+  // after them, so old and new contents never live at once)
+  auto load_rows = [&](Pre& P, double d1 = 0.0, double d2 = 0.0) {
+    const FastStepS& st = sp[after_use(clampk(kr), d1, d2)];
     const double* r = tabj + st.off;
     P.wl = st.wlo;
     P.wh = st.whi;
@@ -1154,17 +1204,16 @@ __device__ __forceinline__ void sweep_group_body(
   auto phaseA = [&](int g, Pre& P, GroupA& A) {
     const int k = Q * g + q;
     A.k = k;
-    // contracted table: mmr = 1, and (0 + a) + b == a + b for its non-negative terms
-    const double kap = (P.vlo * P.wl + P.vhi * P.wh) + sig;
-    const double dm = P.dm, iTnew = P.iT;
-    ring_fence();
-    load_rows(P);
-    A.dtau = dm * kap;
-    A.w0 = fm::div(sig, sig + kap);
     // each lane forms its step's new Planck value; the group gathers them and resolves
     // (B1, B2) of its steps in order (emit: B2 is new and becomes the next B1; absorb: B1 is
     // new and becomes the next B2; emit's top step keeps B2 = B1)
-    const double X = planck(c1, hcl, iTnew, ek);
+    const double X = planck(c1, hcl, P.iT, ek);
+    // contracted table: mmr = 1, and (0 + a) + b == a + b for its non-negative terms
+    const double kap = (P.vlo * P.wl + P.vhi * P.wh) + sig;
+    A.dtau = P.dm * kap;
+    ring_fence();
+    load_rows(P, A.dtau, X);
+    A.w0 = fm::div(sig, sig + kap);
     // the step before this lane's holds the lane before it in the group (quad_perm
     // [0,0,2,2] for Q = 2, [0,0,1,2] for Q = 4), the group's first step the carried value;
     // emit's top step keeps B2 = B1 (it is the last step, so no later step reads it)
@@ -1257,10 +1306,12 @@ __device__ __forceinline__ void sweep_group_body(
   };
   const int ng = (ns + Q - 1) / Q;
   Pre pa, pb;                      // two groups in flight (4: measured no faster)
-  load_rows(pa);
-  load_stale(pa);
+  load_rows(pa);   // rows, then stale fluxes: the loop's own refill order (vmcnt is in order)
   load_rows(pb);
+  ring_fence();
+  load_stale(pa);
   load_stale(pb);
+  ring_fence();
   for (int g = 0; g < ng; g += 2) {
     // 8 waves: two per SIMD from ONE block, held level by a barrier every two group pairs —
     // left alone, the older wave takes the issue slots first and the younger one finishes
@@ -1281,6 +1332,7 @@ __device__ __forceinline__ void sweep_group_body(
       coef_from<true>(A1.w0, A1.dtau, A1.B1, A1.B2, c1);
     }
     finish(A0, c0, pa.stale);
+    consume(pb.stale);
     if (g + 1 < ng) finish(A1, c1, pb.stale);
     ring_fence();
     load_stale(pa);
