@@ -65,9 +65,27 @@ __device__ unsigned int g_trace_n;
 // (hc / (lam k)) * (1 / T) — a per-wavelength constant (host) times a per-layer one (the step
 // record) — instead of one division per update: within 1.5 ulp of the reference's
 // hc / ((lam k) T), which moves spectra and T by < 1e-13.
+//
+// FREI_PLANCK_EXP (default 1): the same value as c1 e / (1 - e) with e = exp(-x), from the
+// transmission's exp (its coefficients are wave-uniform SGPR constants the sweep already holds)
+// instead of an expm1 whose ten coefficients occupied 20 VGPRs per lane: four VALU and 20 VGPRs
+// fewer per update, no range guard (e in [0, 1]: the quotient never overflows, and e underflows
+// to the reference's 0 at x > 745).  Error: a few ulp, growing as ~1 ulp / x for x < 1 (the
+// cancellation in 1 - e) — 1e-15 relative at x = 0.1, far inside the 1e-10 parity bar.  A NaN
+// temperature propagates.  Between x = 709.8 (where numpy's expm1 overflows, B = 0) and 745 it
+// returns the subnormal c1 e instead of 0.
+#ifndef FREI_PLANCK_EXP
+#define FREI_PLANCK_EXP 1
+#endif
+__device__ __forceinline__ double planck_e(double c1, double x) {
+  const double e = fm::exp_neg_unclamped(-x);
+  return fm::div(c1 * e, 1.0 - e);
+}
 __device__ __forceinline__ double planck(double c1, double hcl, double iT) {
 #ifdef FREI_MEMONLY
   return c1 * hcl * iT;
+#elif FREI_PLANCK_EXP
+  return planck_e(c1, hcl * iT);
 #else
   return fm::div_big(c1, fm::expm1(hcl * iT));
 #endif
@@ -85,7 +103,10 @@ __device__ __forceinline__ double planck(double c1, double hcl, double iT) {
 // the guard-free division could lose the denormal quotient.
 __device__ __forceinline__ double planck(double c1, double hcl, double iT,
                                         const fm::Expm1Reg& k) {
-#if FREI_EXPM1_VREG && !defined(FREI_MEMONLY)
+#if FREI_PLANCK_EXP && !defined(FREI_MEMONLY)
+  (void)k;
+  return planck_e(c1, hcl * iT);
+#elif FREI_EXPM1_VREG && !defined(FREI_MEMONLY)
   const double x = hcl * iT;
   double B = fm::div(c1, fm::expm1_mid(x < 600.0 ? x : 600.0, k));
   if (__builtin_expect(!(x <= 600.0), 0)) B = c1 / fm::expm1(x, k);
@@ -409,6 +430,9 @@ __device__ __forceinline__ double stream_load(const double* p) {
 #endif
 }
 
+#ifndef FREI_PRIO_PROGRESS
+#define FREI_PRIO_PROGRESS 1
+#endif
 // Scheduling fence of the sweep's load ring (FREI_RING_FENCE=0: none, A/B).
 #ifndef FREI_RING_FENCE
 #define FREI_RING_FENCE 1
@@ -603,6 +627,39 @@ __device__ __forceinline__ void coef_e1(double w0, double dtau, double B1, doubl
 #endif
 }
 
+// The E-dependent head of a step's coefficients (sq = sqrt(E (E - w0)), r = sqrt((E - w0) / E),
+// q = B' / 2E, pi_w) ahead of the shared coef_tail: the E = 1 values for every lane, then — in a
+// wave-uniform branch taken only when some lane has w0 > 0.1 — coef_from's values on those
+// lanes.  The same bits as coef_e1 / coef_from on every lane, with ONE tail in the loop: the
+// tail duplicated in both branches had set the sweep's register budget (12 VGPRs).
+struct CoefHead {
+  double sq, r, q, pi_w;
+};
+__device__ __forceinline__ CoefHead coef_head_e1(double w0, double dtau, double B1, double B2) {
+  CoefHead h;
+  const double Emw = 1.0 - w0;
+  h.sq = fm::sqrt_pos(Emw);
+  h.r = h.sq;
+  h.q = fm::div(B1 - B2, dtau) * 0.5;   // = div(div(B1 - B2, dtau), 2 E) at E = 1
+#if FREI_PI_E1 || FREI_LEAN
+  h.pi_w = kPi;
+#else
+  h.pi_w = fm::div(kPi * (1.0 - w0), Emw);
+#endif
+  return h;
+}
+__device__ __forceinline__ void coef_head_general(double w0, double dtau, double B1, double B2,
+                                                  CoefHead& h) {
+  if (w0 > 0.1) {
+    const double E = (1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0);
+    const double Emw = E - w0;
+    h.q = fm::div(fm::div(B1 - B2, dtau), 2.0 * E);
+    h.pi_w = fm::div(kPi * (1.0 - w0), Emw);
+    h.sq = fm::sqrt_pos(E * Emw);
+    h.r = fm::sqrt_pos(fm::div(Emw, E));
+  }
+}
+
 struct PreCoef {
   double w0, dtau, B1, B2;
 };
@@ -731,6 +788,12 @@ __device__ __forceinline__ void sweep_fast_body(
   static_assert(PD == 1 || PD == 2 || PD == 4, "prefetch depth 1, 2 or 4");
   static_assert(PF % PD == 0, "prefetch distance: a multiple of the coefficient block");
   static_assert(!MM1 || S == 1, "mmr = 1 only for the contracted single table");
+  // staged partial sums (red_rows 2) reduce a pair of steps: the pair is one coefficient block
+  // (PD = 2), or the two one-step blocks of a trip (PD = 1, PF = 2: fewer registers per wave)
+  constexpr bool kPairs = PD == 2 || (PD == 1 && PF == 2);
+#if defined(FREI_ISA_E1ONLY) || defined(FREI_ISA_STAGED)   // ISA-histogram build: the staged partial sums, as the 500k sweep runs
+  a.red_rows = 2;
+#endif
   // no NaN reaches the coefficients: the contracted table is built from NaN-free tables, and
   // with S > 1 the tables were scanned (NaN-free, or NANCHK's nansum zeroes NaN terms); only a
   // single per-species table keeps the reference's NaN propagation (Q8)
@@ -901,20 +964,27 @@ __device__ __forceinline__ void sweep_fast_body(
     }
 #else
     bool e1 = true;
+    CoefHead h[PD];
 #pragma unroll
-    for (int b = 0; b < PD; ++b) e1 = e1 && !(pc[b].w0 > 0.1);
+    for (int b = 0; b < PD; ++b) {
+      e1 = e1 && !(pc[b].w0 > 0.1);
+      h[b] = coef_head_e1(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2);
+    }
 #ifdef FREI_ISA_E1ONLY   // ISA-histogram build (tools/isa_hist.py): the E = 1 path alone
     e1 = true;
 #endif
-    if (__all(e1)) {
+    if (!__all(e1)) {   // rare: one step at a time (registers, not ILP)
 #pragma unroll
-      for (int b = 0; b < PD; ++b)
-        coef_e1<kNaNFree>(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2, c[b]);
-    } else {
-#pragma unroll
-      for (int b = 0; b < PD; ++b)
-        coef_from<kNaNFree>(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2, c[b]);
+      for (int b = 0; b < PD; ++b) {
+        ring_fence();
+        coef_head_general(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2, h[b]);
+      }
+      ring_fence();
     }
+#pragma unroll
+    for (int b = 0; b < PD; ++b)
+      coef_tail<kNaNFree>(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2, h[b].sq, h[b].r, h[b].q,
+                          h[b].pi_w, c[b]);
 #endif
   };
 
@@ -939,7 +1009,7 @@ __device__ __forceinline__ void sweep_fast_body(
       if (st_dn) flux_store(Fd + (int64_t)i * nl + j, F1d);
       if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = c.dtau;
     }
-    if (PD == 2 && a.red_rows == 2) {   // staged: reduced per pair of steps (stage_reduce)
+    if (kPairs && a.red_rows == 2) {   // staged: reduced per pair of steps (stage_reduce)
       double* t = red + (int64_t)(kBlock / 64) * ns * 4 + ((wv * 2 + (k & 1)) * 4) * kStageRow +
                   lane;
       t[0] = wt * F2u;
@@ -993,10 +1063,24 @@ __device__ __forceinline__ void sweep_fast_body(
   for (int b = 0; b < PF; ++b) load_stale(b, sb[b]);
   ring_fence();
   for (int k0 = 0; k0 < ns; k0 += PF) {
+#if FREI_PRIO_PROGRESS
+    // issue priority by progress (diagnostic A/B): a wave early in its layer loop outranks one
+    // near its end, so waves that started late (second-round blocks) catch up instead of
+    // trailing alone at the end of the launch (the hardware otherwise favours the oldest wave)
+    switch ((4 * k0) / ns) {
+      case 0: __builtin_amdgcn_s_setprio(3); break;
+      case 1: __builtin_amdgcn_s_setprio(2); break;
+      case 2: __builtin_amdgcn_s_setprio(1); break;
+      default: __builtin_amdgcn_s_setprio(0); break;
+    }
+#endif
 #pragma unroll
   for (int g = 0; g < PF / PD; ++g) {
     const int k = k0 + g * PD;
-    if (PF > PD && k >= ns) break;   // wave-uniform: no dummy coefficient blocks at the end
+    // wave-uniform: no dummy coefficient blocks at the end (a pair's dummy second step runs,
+    // unstored, so the pair's reduction below sees both steps)
+    if (PF > PD && !(PD == 1 && kPairs) && k >= ns) break;
+    if constexpr (PD == 1 && kPairs) ring_fence();   // one step at a time: registers, not ILP
     StepCoef c[PD];
     PreCoef pc[PD];
     double tot[PD], X[PD];
@@ -1020,8 +1104,10 @@ __device__ __forceinline__ void sweep_fast_body(
     ring_fence();
 #pragma unroll
     for (int b = 0; b < PD; ++b) load_stale(k + b + PF, sb[g * PD + b]);
-    if constexpr (PD == 2) {
-      if (a.red_rows == 2) {   // the pair's 8 (step, quantity) sums over the wave's 64 lanes
+    if constexpr (kPairs) {
+      // the pair's 8 (step, quantity) sums over the wave's 64 lanes, once both are staged
+      if (a.red_rows == 2 && (PD == 2 || (g & 1))) {
+        const int kp = PD == 2 ? k : k - 1;   // the pair's first step
         __builtin_amdgcn_wave_barrier();
         const int o = lane >> 3;
         // lane r = lane & 7 of output o sums lanes r, r + 8, ..., r + 56 of that output's row
@@ -1033,7 +1119,7 @@ __device__ __forceinline__ void sweep_fast_body(
         y += dpp_bcast<0xB1>(y);    // quad_perm [1,0,3,2]
         y += dpp_bcast<0x4E>(y);    // quad_perm [2,3,0,1]
         y += dpp_bcast<0x141>(y);   // row_half_mirror: the other quad of the 8-lane group
-        const int ks = k + (o >> 2);
+        const int ks = kp + (o >> 2);
         if ((lane & 7) == 0 && ks < ns) red[((int64_t)wv * ns + ks) * 4 + (o & 3)] = y;
         __builtin_amdgcn_wave_barrier();
       }
@@ -1324,13 +1410,15 @@ __device__ __forceinline__ void sweep_group_body(
     phaseA(g, pa, A0);
     phaseA(g + 1, pb, A1);   // a dummy group past the end is computed, not stored
     StepCoef c0, c1;
-    if (__all(!(A0.w0 > 0.1) && !(A1.w0 > 0.1))) {
-      coef_e1<true>(A0.w0, A0.dtau, A0.B1, A0.B2, c0);   // contracted table: NaN-free
-      coef_e1<true>(A1.w0, A1.dtau, A1.B1, A1.B2, c1);
-    } else {
-      coef_from<true>(A0.w0, A0.dtau, A0.B1, A0.B2, c0);
-      coef_from<true>(A1.w0, A1.dtau, A1.B1, A1.B2, c1);
+    CoefHead h0 = coef_head_e1(A0.w0, A0.dtau, A0.B1, A0.B2);
+    CoefHead h1 = coef_head_e1(A1.w0, A1.dtau, A1.B1, A1.B2);
+    if (!__all(!(A0.w0 > 0.1) && !(A1.w0 > 0.1))) {
+      coef_head_general(A0.w0, A0.dtau, A0.B1, A0.B2, h0);
+      coef_head_general(A1.w0, A1.dtau, A1.B1, A1.B2, h1);
     }
+    // contracted table: NaN-free
+    coef_tail<true>(A0.w0, A0.dtau, A0.B1, A0.B2, h0.sq, h0.r, h0.q, h0.pi_w, c0);
+    coef_tail<true>(A1.w0, A1.dtau, A1.B1, A1.B2, h1.sq, h1.r, h1.q, h1.pi_w, c1);
     finish(A0, c0, pa.stale);
     consume(pb.stale);
     if (g + 1 < ng) finish(A1, c1, pb.stale);
@@ -1596,14 +1684,19 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
         }
       } else
 #endif
-      if (__all(e1)) {
+      {
+        CoefHead h[M];
+#pragma unroll
+        for (int i = 0; i < M; ++i) h[i] = coef_head_e1(pc[i].w0, pc[i].dtau, pc[i].B1, pc[i].B2);
+        if (!__all(e1)) {
+#pragma unroll
+          for (int i = 0; i < M; ++i)
+            coef_head_general(pc[i].w0, pc[i].dtau, pc[i].B1, pc[i].B2, h[i]);
+        }
 #pragma unroll
         for (int i = 0; i < M; ++i)   // contracted table: NaN-free
-          coef_e1<true>(pc[i].w0, pc[i].dtau, pc[i].B1, pc[i].B2, c[i]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < M; ++i)
-          coef_from<true>(pc[i].w0, pc[i].dtau, pc[i].B1, pc[i].B2, c[i]);
+          coef_tail<true>(pc[i].w0, pc[i].dtau, pc[i].B1, pc[i].B2, h[i].sq, h[i].r, h[i].q,
+                          h[i].pi_w, c[i]);
       }
 #pragma unroll
       for (int i = 0; i < M; ++i) {
@@ -2328,6 +2421,9 @@ __device__ __forceinline__ void update_arrive(const UpdateArgs& a, int nU, int i
 // half past the last layer (lr >= n_layers, odd layer counts) computes the last layer again
 // with every side effect suppressed, so both halves meet the same block barriers.
 // sh: dynamic LDS of (2 n_layers + n_tnodes) doubles.
+// U: partial-sum strides loaded per batch (the standalone update kernel; a chained launch's
+// update blocks share the sweep's register budget and keep U = 1)
+template <int U = 1>
 __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, int h,
                                   double* sh) {
 #ifdef FREI_UPD_EMPTY  // diagnostic ablation build: launch floor
@@ -2401,9 +2497,32 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
     }
     double acc[8];
     for (int j = 0; j < 8; ++j) acc[j] = 0.0;
+    // U strided partials of all 8 rows loaded before any is added (one round trip per batch,
+    // not per two strides: the previous trip's adds no longer gate the next loads), then
+    // added in the same order as before — per thread b = tid, tid + 256, ... — so the sums
+    // keep reduce_kernel's bits.  Past the end the loads repeat the last block (in bounds)
+    // and are not added.  (500k: 1954 blocks, 8 strides, 64 loads in flight per thread.)
+    constexpr int kU = U;
+    const int nb = a.nblocks;
+    if constexpr (U == 1) {
 #pragma unroll 2
-    for (int b = tid; b < a.nblocks; b += kRedThreads)
-      for (int j = 0; j < 8; ++j) acc[j] += pj[j][b];
+      for (int b = tid; b < nb; b += kRedThreads)
+        for (int j = 0; j < 8; ++j) acc[j] += pj[j][b];
+    } else
+    for (int b0 = tid; b0 < nb; b0 += kU * kRedThreads) {
+      double v[kU][8];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int b = min(b0 + u * kRedThreads, nb - 1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[u][j] = pj[j][b];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (b0 + u * kRedThreads < nb)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += v[u][j];
+    }
     for (int j = 0; j < 8; ++j)
       acc[j] = butterfly_sum(acc[j], tid & 63);   // = the xor-32 ... 1 shfl butterfly
     if ((tid & 63) == 0)
@@ -2532,9 +2651,12 @@ __device__ __forceinline__ void update_shadow(const UpdateArgs& a) {
   __syncthreads();
 }
 
+#ifndef FREI_UPD_BATCH
+#define FREI_UPD_BATCH 8
+#endif
 __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sh[];
-  update_fused_body(a, blockIdx.x, gridDim.x, threadIdx.x, 0, sh);
+  update_fused_body<FREI_UPD_BATCH>(a, blockIdx.x, gridDim.x, threadIdx.x, 0, sh);
 }
 
 // Chained launch: workgroups [0, nU) run the previous sweep's fused update (u; with 8-wave
@@ -3188,6 +3310,12 @@ static void launch_fast_sh(int dir, int S, int depth, int pf, bool nan_check, co
       if (dir == kEmit) launch_fast_pf<kEmit, 2, SH>(pf, a, nblocks, st);
       else launch_fast_pf<kAbsorb, 2, SH>(pf, a, nblocks, st);
     }
+    return;
+  }
+  if (depth == 1 && pf == 2 && S == 1 && a.unit_mmr && !nan_check) {
+    // one step per coefficient block, loads two steps ahead (fewer registers: 5 waves per SIMD)
+    if (dir == kEmit) launch_fast_t<kEmit, 1, 1, false, SH, true, 2>(a, nblocks, st);
+    else launch_fast_t<kAbsorb, 1, 1, false, SH, true, 2>(a, nblocks, st);
     return;
   }
   if (depth >= 4 && S == 1 && !nan_check) {  // 4 steps in flight: small slices, one table

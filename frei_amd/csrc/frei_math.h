@@ -231,6 +231,27 @@ __device__ __forceinline__ double exp_neg_nf(double x) {
   return __builtin_ldexp(p, (int)n);
 }
 
+// exp(x) for x <= 0 without the clamp (Planck factors, frei_kernels.hip planck_e): exp_neg's
+// sequence, so bit-identical to it for x in [-1100, 0]; below, n stays an int32 and the final
+// ldexp still underflows to 0.  NaN propagates; x = -inf gives NaN (a zero temperature).
+__device__ __forceinline__ double exp_neg_unclamped(double x) {
+  const double n = __builtin_rint(x * c64(0x3ff71547652b82feull));
+  double r = __builtin_fma(c64(0xbfe62e42fefa39efull), n, x);
+  r = __builtin_fma(c64(0xbc7abc9e3b39803full), n, r);
+  double p = __builtin_fma(c64(0x3e5ade156a5dcb37ull), r, c64(0x3e928af3fca7ab0cull));
+  p = hfma(r, p, 0x3ec71dee623fde64ull);
+  p = hfma(r, p, 0x3efa01997c89e6b0ull);
+  p = hfma(r, p, 0x3f2a01a014761f6eull);
+  p = hfma(r, p, 0x3f56c16c1852b7b0ull);
+  p = hfma(r, p, 0x3f81111111122322ull);
+  p = hfma(r, p, 0x3fa55555555502a1ull);
+  p = hfma(r, p, 0x3fc5555555555511ull);
+  p = hfma(r, p, 0x3fe000000000000bull);
+  p = __builtin_fma(r, p, 1.0);
+  p = __builtin_fma(r, p, 1.0);
+  return __builtin_ldexp(p, (int)n);
+}
+
 // 1 / b within one ulp: the reciprocal part of the division core below (rcp and two
 // Newton-Raphson steps) without the quotient's final residual correction.  Used where the
 // result only scales a sum (1 / chi of the flux update), so an ulp is not amplified.

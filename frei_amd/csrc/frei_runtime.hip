@@ -791,13 +791,15 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
     const int depth = c->prefetch_depth > 0 ? c->prefetch_depth
                       : (S_run == 1 && c->nblocks <= c->depth4_max_blocks) ? 4 : 2;
     // loads issued pf steps ahead (the contracted table only; 0: the coefficient block's depth)
-    const int pf = (c->eff && S_run == 1 && depth >= 2) ? c->prefetch_steps : 0;
+    // (prefetch_steps 2 with depth 1: one step per coefficient block, loads two steps ahead)
+    const int pf = (c->eff && S_run == 1 && (depth >= 2 || c->prefetch_steps == 2))
+                       ? c->prefetch_steps : 0;
     bool nan_check = false;
     for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
     const int Q = group_lanes(c);
     // staged partial sums (mode 2): the one-lane sweep with two steps in flight, and the
     // grouped-lane sweep (two groups in flight)
-    if ((Q > 1 || depth == 2) && c->red_stage &&
+    if ((Q > 1 || depth == 2 || (depth == 1 && pf == 2)) && c->red_stage &&
         ((size_t)(kBlock / 64) * ns * 4 + (size_t)(kBlock / 64) * 2 * 4 * 72) * sizeof(double) +
                 (size_t)ns * sizeof(FastStepS) <= 48 * 1024)
       f.red_rows = 2;
@@ -1043,7 +1045,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "group_waves") c->group_waves = v == 8 ? 8 : 4;
   else if (k == "chain") c->chain = v < 0 ? 0 : (v > 2 ? 2 : v);
   else if (k == "sweep_lds_kb") c->sweep_lds_kb = v < 0 ? 0 : (v > 160 ? 160 : v);
-  else if (k == "prefetch_steps") c->prefetch_steps = v >= 16 ? 16 : v >= 8 ? 8 : 0;
+  else if (k == "prefetch_steps") c->prefetch_steps = v >= 16 ? 16 : v >= 8 ? 8 : v == 2 ? 2 : 0;
   else return fail("unknown option '" + k + "'");
   c->meta_dirty = true;
   return 0;
