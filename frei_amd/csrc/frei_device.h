@@ -387,6 +387,9 @@ __host__ __device__ inline size_t update_lds_bytes(int nL, int ntn, int S, bool 
 void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st);
 void launch_sweep_fast(int dir, int S, int depth, int pf, bool nan_check, bool shared,
                        const FastArgs& a, int nblocks, hipStream_t st);
+// The contracted one-lane sweep with two adjacent wavelengths per lane (even n_lam, global step
+// records, staged partial sums: a.red_rows = 2); nblocks = ceil(n_lam / (2 kBlock)).
+void launch_sweep_pair(int dir, const FastArgs& a, int nblocks, hipStream_t st);
 // Grouped-lane sweep (Q = 2 or 4 lanes per wavelength, NW = 4 or 8 waves per block, 64 NW / Q
 // wavelengths per block):
 // contracted single table, step table in LDS; for slices with about one wave per SIMD.

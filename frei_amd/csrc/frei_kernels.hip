@@ -1466,6 +1466,206 @@ __global__ __launch_bounds__(64 * NW) void sweep_group_kernel(
 }
 
 
+// ---------------------------------------------------------------- K1, two wavelengths per lane
+// The contracted one-table sweep (K3) with each lane carrying two adjacent wavelengths: half the
+// waves of the one-lane form, so a 500k-lambda launch (3908 waves) is ONE round of the 4096
+// wave slots at four waves per SIMD instead of 1.5 rounds of the one-lane form's five: no
+// second-round blocks that start late and finish alone (measured: the one-lane sweep takes
+// 0.40 ns per lambda at whole rounds, 0.41-0.43 ns at 1.25-1.5 rounds, profiles/r04/c8/rounds.txt).
+// Every wavelength's flux recurrence is the one-lane form's, expression for expression (fluxes
+// bit-identical); the two wavelengths' weighted bolometric terms are added in the lane first
+// (fma(wt_b, F_b, wt_a F_a)) and then go through the one-lane form's staged reduction, so the
+// partial sums follow this form's own fixed tree and each block writes half as many partials.
+// 16-byte loads and stores (the pair is adjacent in every row; the host requires an even n_lam
+// and the tables' pitch is even).  Loads two steps ahead (the one-lane ring), one step per
+// coefficient block per wavelength (the two wavelengths are the block's two chains).
+template <int DIR>
+__global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
+    FastArgs a, const FastStep* __restrict__ st, double* __restrict__ Fu,
+    double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
+  extern __shared__ double red[];
+  using d2 = double2;
+  {  // atmosphere of a batched launch (identity for one atmosphere)
+    const int m = blockIdx.y;
+    Fu += m * a.bs.flux;
+    Fd += m * a.bs.flux;
+    part += m * a.bs.part;
+    if (dtaus) dtaus += m * a.bs.flux;
+    st += m * a.bs.steps;
+    a.tab[0] += m * a.bs.tab;
+    a.ftoa += m * a.bs.ftoa;
+    a.conv += m;
+  }
+  if (!a.force && *a.conv) return;
+  TRACE_DECL;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int bx = blockIdx.x, nbx = gridDim.x;
+  const int64_t nl = a.n_lam;
+  const int ns = a.n_steps;
+  const int64_t j0 = 2 * ((int64_t)bx * kBlock + tid);   // the lane's first wavelength
+  const bool act = j0 < nl;
+  const int64_t j = act ? j0 : nl - 2;
+  auto ld2 = [](const double* p) { return *reinterpret_cast<const d2*>(p); };
+  auto st2 = [](double* p, d2 v) { *reinterpret_cast<d2*>(p) = v; };
+  const d2 c1 = ld2(a.c1 + j), hcl = ld2(a.hcl + j), sig = ld2(a.sig + j);
+  const d2 wt = act ? ld2(a.wtr + j) : d2{0.0, 0.0};
+  TRACE_MARK(1);
+  auto layer_of = [&](int k) { return step_layer(DIR, k, ns + 1); };
+  auto top_of = [&](int k) { return DIR == kEmit && k == ns - 1; };
+  auto clampk = [&](int k) { return k < ns ? k : ns - 1; };
+  auto load_rows = [&](int k, d2 (&v)[2], double dep1 = 0.0, double dep2 = 0.0) {
+    const double* r = a.tab[0] + after_use(st[clampk(k)].off[0] + j, dep1, dep2);
+    v[0] = ld2(r);
+    v[1] = ld2(r + a.pitch);
+  };
+  auto load_stale = [&](int k, d2& stale) {
+    k = clampk(k);
+    const int i = layer_of(k);
+    const double* src = (DIR == kEmit) ? (top_of(k) ? a.ftoa : Fd + (int64_t)(i + 1) * nl)
+                                       : Fu + (int64_t)i * nl;
+    stale = ld2(src + j);
+  };
+  d2 carry, Bc;
+  {
+    const int l0 = st[0].layer;
+    const double iT = DIR == kEmit ? st[0].iT1 : st[0].iT2;
+    carry = ld2((DIR == kEmit ? Fu + (int64_t)l0 * nl : Fd + (int64_t)(l0 + 1) * nl) + j);
+    Bc = d2{planck(c1.x, hcl.x, iT), planck(c1.y, hcl.y, iT)};
+  }
+  d2 vb[2][2], sb[2];
+  load_rows(0, vb[0]);   // rows first, then the stale fluxes (the loop's refill order)
+  load_rows(1, vb[1]);
+  ring_fence();
+  load_stale(0, sb[0]);
+  load_stale(1, sb[1]);
+  ring_fence();
+  double* tile = red + (int64_t)(kBlock / 64) * ns * 4;
+  for (int k0 = 0; k0 < ns; k0 += 2) {
+#if FREI_PRIO_PROGRESS
+    switch ((4 * k0) / ns) {
+      case 0: __builtin_amdgcn_s_setprio(3); break;
+      case 1: __builtin_amdgcn_s_setprio(2); break;
+      case 2: __builtin_amdgcn_s_setprio(1); break;
+      default: __builtin_amdgcn_s_setprio(0); break;
+    }
+#endif
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {   // step k0 + 1 past the end: a dummy, computed, not stored
+      const int k = k0 + g;
+      const int kk = clampk(k);
+      ring_fence();
+      const FastStep& sk = st[kk];
+      const double iTn = DIR == kEmit ? sk.iT2 : sk.iT1;
+      const d2 X = {planck(c1.x, hcl.x, iTn), planck(c1.y, hcl.y, iTn)};
+      // contracted table: mmr = 1, and (0 + a) + b == a + b for its non-negative terms
+      const double wl = sk.wlo[0], wh = sk.whi[0], dm = sk.dm;
+      const d2 tot = {vb[g][0].x * wl + vb[g][1].x * wh, vb[g][0].y * wl + vb[g][1].y * wh};
+      ring_fence();
+      load_rows(k + 2, vb[g], tot.x, tot.y);
+      const bool top = top_of(kk);
+      PreCoef pa, pb;
+      {
+        const double ka = tot.x + sig.x, kb = tot.y + sig.y;
+        pa.dtau = dm * ka;
+        pb.dtau = dm * kb;
+        pa.w0 = fm::div(sig.x, sig.x + ka);
+        pb.w0 = fm::div(sig.y, sig.y + kb);
+      }
+      if (DIR == kEmit) {
+        pa.B1 = Bc.x; pa.B2 = top ? Bc.x : X.x;
+        pb.B1 = Bc.y; pb.B2 = top ? Bc.y : X.y;
+        Bc = d2{pa.B2, pb.B2};
+      } else {
+        pa.B2 = Bc.x; pa.B1 = X.x;
+        pb.B2 = Bc.y; pb.B1 = X.y;
+        Bc = X;
+      }
+      CoefHead ha = coef_head_e1(pa.w0, pa.dtau, pa.B1, pa.B2);
+      CoefHead hb = coef_head_e1(pb.w0, pb.dtau, pb.B1, pb.B2);
+      bool e1 = !(pa.w0 > 0.1) && !(pb.w0 > 0.1);
+#ifdef FREI_ISA_E1ONLY
+      e1 = true;
+#endif
+      if (!__all(e1)) {   // rare: one wavelength at a time (registers, not ILP)
+        ring_fence();
+        coef_head_general(pa.w0, pa.dtau, pa.B1, pa.B2, ha);
+        ring_fence();
+        coef_head_general(pb.w0, pb.dtau, pb.B1, pb.B2, hb);
+        ring_fence();
+      }
+      StepCoef ca, cb;
+      coef_tail<true>(pa.w0, pa.dtau, pa.B1, pa.B2, ha.sq, ha.r, ha.q, ha.pi_w, ca);
+      coef_tail<true>(pb.w0, pb.dtau, pb.B1, pb.B2, hb.sq, hb.r, hb.q, hb.pi_w, cb);
+      // finish: the carried recurrence of both wavelengths, stores, staged weighted terms
+      const d2 Fst = sb[g];
+      consume(Fst.x);
+      consume(Fst.y);
+      const d2 F1u = (DIR == kEmit) ? carry : Fst, F2d = (DIR == kEmit) ? Fst : carry;
+      const d2 F2u = {step_up(ca.psi, ca.xi, ca.ic, ca.Xu, F1u.x, F2d.x),
+                      step_up(cb.psi, cb.xi, cb.ic, cb.Xu, F1u.y, F2d.y)};
+      const d2 F1d = {step_dn(ca.psi, ca.xi, ca.ic, ca.Xd, F1u.x, F2d.x),
+                      step_dn(cb.psi, cb.xi, cb.ic, cb.Xd, F1u.y, F2d.y)};
+      if (k < ns) {
+        const int i = layer_of(k);
+        if (act) {
+          const bool st_up = (DIR == kEmit) ? !top : (!a.live_only || i == 0);
+          const bool st_dn = (DIR == kAbsorb) || !a.live_only || top;
+          if (st_up) st2(Fu + (int64_t)(i + 1) * nl + j, F2u);
+          if (st_dn) st2(Fd + (int64_t)i * nl + j, F1d);
+          if (dtaus) st2(dtaus + (int64_t)(k + 1) * nl + j, d2{ca.dtau, cb.dtau});
+        }
+        double* t = tile + ((wv * 2 + (k & 1)) * 4) * kStageRow + lane;
+        t[0] = __builtin_fma(wt.y, F2u.y, wt.x * F2u.x);
+        t[kStageRow] = __builtin_fma(wt.y, F2d.y, wt.x * F2d.x);
+        t[2 * kStageRow] = __builtin_fma(wt.y, F1u.y, wt.x * F1u.x);
+        t[3 * kStageRow] = __builtin_fma(wt.y, F1d.y, wt.x * F1d.x);
+        carry = (DIR == kEmit) ? F2u : F1d;
+      }
+      ring_fence();
+      load_stale(k + 2, sb[g]);
+    }
+    // the pair's 8 (step, quantity) sums over the wave's 64 lanes (the one-lane form's stage)
+    __builtin_amdgcn_wave_barrier();
+    const int o = lane >> 3;
+    const double* t = tile + ((wv * 2 + (o >> 2)) * 4 + (o & 3)) * kStageRow + (lane & 7);
+    double y = t[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) y += t[8 * i];
+    y += dpp_bcast<0xB1>(y);    // quad_perm [1,0,3,2]
+    y += dpp_bcast<0x4E>(y);    // quad_perm [2,3,0,1]
+    y += dpp_bcast<0x141>(y);   // row_half_mirror: the other quad of the 8-lane group
+    const int ks = k0 + (o >> 2);
+    if ((lane & 7) == 0 && ks < ns) red[((int64_t)wv * ns + ks) * 4 + (o & 3)] = y;
+    __builtin_amdgcn_wave_barrier();
+  }
+  TRACE_MARK(2);
+  __syncthreads();
+  for (int idx = tid; idx < ns * 4; idx += kBlock) {
+    double sum = red[idx];
+    for (int w = 1; w < kBlock / 64; ++w) sum += red[(int64_t)w * ns * 4 + idx];
+    part[(int64_t)idx * nbx + bx] = sum;
+  }
+  TRACE_PUT(2);
+}
+
+static size_t sweep_shm(const void* kernel, const FastArgs& a, size_t shm);
+// Two wavelengths per lane (sweep_pair_kernel): nblocks = ceil(n_lam / 512).
+void launch_sweep_pair(int dir, const FastArgs& a, int nblocks, hipStream_t st) {
+  const size_t shm = (size_t)red_lds_doubles(2, a.n_steps) * sizeof(double);
+  const dim3 grid(nblocks, a.n_atm > 1 ? a.n_atm : 1);
+  if (dir == kEmit) {
+    const auto k = sweep_pair_kernel<kEmit>;
+    hipLaunchKernelGGL(k, grid, dim3(kBlock), sweep_shm(reinterpret_cast<const void*>(k), a, shm),
+                       st, a, a.steps, a.F_up, a.F_down, a.part, a.dtaus);
+  } else {
+    const auto k = sweep_pair_kernel<kAbsorb>;
+    hipLaunchKernelGGL(k, grid, dim3(kBlock), sweep_shm(reinterpret_cast<const void*>(k), a, shm),
+                       st, a, a.steps, a.F_up, a.F_down, a.part, a.dtaus);
+  }
+}
+
 // Dynamic LDS of a one-lane / grouped-lane sweep launch: at least a.min_lds bytes
 // (FREI_SWEEP_LDS_KB), which caps the blocks resident per CU at 160 KiB / min_lds, so the
 // dispatcher cannot stack three or four blocks on one CU while others hold one (small slices:

@@ -220,6 +220,8 @@ struct frei_ctx {
   int pipe_pf = 1;                      // FREI_PIPE_PF: phases the producers load ahead (1, 2)
   int red_rows = 1;                     // FREI_RED_ROWS=0: full wave sums per step
   int red_stage = 1;                    // FREI_RED_STAGE=0: no staged sums (one-lane sweep)
+  int lam2 = -1;                        // FREI_LAM2: two wavelengths per lane in the contracted
+                                        // one-lane sweep (1 on, 0 off, -1 large slices)
   int sweep_lds_kb = 0;                 // FREI_SWEEP_LDS_KB: minimum LDS per sweep block (KiB)
   int group_waves = 4;                  // FREI_GROUP_WAVES: waves per grouped-lane sweep block
   int depth4_max_blocks = 0;            // FREI_DEPTH4_MAX_BLOCKS (4 steps in flight: off, measured no faster)
@@ -563,6 +565,10 @@ SetupArgs setup_args(frei_ctx* c);
 // Sweeps form their own step records in their prologue (and the update kernels skip writing
 // them) when the sweep reads the shared-bracket records from LDS — every form on the contracted
 // table with shared brackets — and the mixing ratios are fixed (no T-dependent chemistry).
+// two wavelengths per lane from this many one-lane blocks (about 1.1 rounds of the one-lane
+// form at five waves per SIMD)
+constexpr int kLam2MinBlocks = 1400;
+
 bool records_in_sweep(frei_ctx* c) {
   if (!(c->rec_sweep && c->fast && c->eff && c->shared && !c->chem_on)) return false;
   // auto: not for batched contexts (every (block, atmosphere) would form the records: C5 -2 %,
@@ -807,10 +813,16 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
     if (Q > 1) nb_run = (int)((c->nlam + 64 * NW / Q - 1) / (64 * NW / Q));
     const int NC = pipe_consumers(c);
     if (NC > 0) nb_run = (int)((c->nlam + 64 * NC - 1) / (64 * NC));
+    // two wavelengths per lane: the one-lane contracted sweep on slices that need more than
+    // about one round of one-lane blocks (1280 resident at five waves per SIMD on 256 CUs)
+    const bool lam2 = c->lam2 != 0 && c->eff && S_run == 1 && !c->shared && !nan_check &&
+                      Q == 1 && NC == 0 && !merge && depth == 2 && pf <= 2 && f.red_rows == 2 &&
+                      c->nlam % 2 == 0 && (c->lam2 > 0 || c->nblocks >= kLam2MinBlocks);
+    if (lam2) nb_run = (int)((c->nlam + 2 * kBlock - 1) / (2 * kBlock));
     if (c->keys) {
       uint64_t h = arg_hash(1469598103934665603ull, f);
-      const int cfg[10] = {o.dir, Q, S_run, depth, (nan_check && !c->eff) ? 1 : 0, c->shared,
-                           NC, c->pipe_pf, pf, NW};
+      const int cfg[11] = {o.dir, Q, S_run, depth, (nan_check && !c->eff) ? 1 : 0, c->shared,
+                           NC, c->pipe_pf, pf, NW, lam2 ? 1 : 0};
       c->keys->push_back(arg_hash(h, cfg));
     }
     if (c->dry) {
@@ -839,6 +851,8 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
       c->has_pend = false;
       launch_sweep_fast_chain(o.dir, depth, pf, f, u, c->nblocks, c->stream);
       ++c->n_chained;
+    } else if (lam2) {
+      launch_sweep_pair(o.dir, f, nb_run, c->stream);
     } else {
       launch_sweep_fast(o.dir, S_run, depth, pf, nan_check && !c->eff, c->shared != 0, f,
                         c->nblocks, c->stream);
@@ -1022,7 +1036,7 @@ const char* const kOptionNames[] = {"prefetch_depth", "shared", "shared_max_bloc
                                     "quad_max_blocks", "red_rows", "red_stage", "group_q",
                                     "fused_update", "graph", "pipe", "pipe_pf", "pipe_min_blocks", "rec_sweep",
                                     "pipe_max_blocks", "prefetch_steps", "k7_mfma", "sweep_lds_kb", "group_waves", "chain",
-                                    nullptr};
+                                    "lam2", nullptr};
 int set_option(frei_ctx* c, const std::string& k, int v) {
   if (k == "prefetch_depth") c->prefetch_depth = v;
   else if (k == "shared") c->shared_mode = v < 0 ? -1 : (v ? 1 : 0);
@@ -1044,6 +1058,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "k7_mfma") c->k7_mfma = v != 0;
   else if (k == "group_waves") c->group_waves = v == 8 ? 8 : 4;
   else if (k == "chain") c->chain = v < 0 ? 0 : (v > 2 ? 2 : v);
+  else if (k == "lam2") c->lam2 = v < 0 ? -1 : (v ? 1 : 0);
   else if (k == "sweep_lds_kb") c->sweep_lds_kb = v < 0 ? 0 : (v > 160 ? 160 : v);
   else if (k == "prefetch_steps") c->prefetch_steps = v >= 16 ? 16 : v >= 8 ? 8 : v == 2 ? 2 : 0;
   else return fail("unknown option '" + k + "'");
@@ -2105,9 +2120,14 @@ int frei_ctx_path(frei_ctx* c, int* flags) {
   for (const auto& q : c->sp) nan = nan || q.has_nan;
   const int Q = group_lanes(c);
   const int NC = pipe_consumers(c);
+  // (the sweep itself also requires a depth-2 coefficient block with staged sums: the defaults)
+  const bool lam2 = c->lam2 != 0 && c->fast && c->eff && !c->shared && Q == 1 && NC == 0 &&
+                    c->nlam % 2 == 0 && (c->lam2 > 0 || c->nblocks >= kLam2MinBlocks) &&
+                    c->prefetch_depth != 1 && c->prefetch_depth < 4 && c->prefetch_steps <= 2 &&
+                    c->red_stage;
   *flags = (c->fast ? 1 : 0) | (c->fast && c->shared ? 2 : 0) | (c->eff ? 4 : 0) |
            (nan ? 8 : 0) | (NC == 0 && Q == 2 ? 16 : 0) | (NC == 0 && Q == 4 ? 32 : 0) |
-           (NC << 6);
+           (NC << 6) | (lam2 ? 512 : 0);
   return 0;
 }
 

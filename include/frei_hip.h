@@ -216,7 +216,8 @@ int frei_contribution(frei_ctx* ctx, const double* dtaus, const double* nu,
  * LDS (shared brackets, small slices), bit 2 species-contracted table (K3), bit 3 tables
  * hold NaN (per-species nansum variant), bit 4 / bit 5 grouped-lane sweep with two / four
  * lanes per wavelength (small slices), bits 6-8: consumer waves per block of the
- * producer/consumer sweep (1, 2 or 4; 0 = not used). */
+ * producer/consumer sweep (1, 2 or 4; 0 = not used), bit 9 two wavelengths per lane in the
+ * contracted one-lane sweep (large slices: option "lam2"). */
 int frei_ctx_path(frei_ctx* ctx, int* flags);
 
 /* Tuning knobs (also FREI_<NAME> in the environment at context creation): "precontract"

@@ -3,8 +3,10 @@
 The oracle cannot run 500k wavelengths in test time, so at BASELINE.json's full size the
 checks are size-independent properties of the path:
 - determinism: two runs give bitwise identical temperatures, spectra and dtaus;
-- the grouped-lane sweep (2 lanes per wavelength, forced) against the one-lane sweep the
-  full slice uses: temperatures within 1e-12 (only the bolometric summation tree differs);
+- the default sweep at this size (two wavelengths per lane, `lam2`) against the one-lane sweep:
+  temperatures within 1e-12 (only the bolometric summation tree differs);
+- the grouped-lane sweep (2 lanes per wavelength, forced) against the one-lane sweep:
+  temperatures within 1e-12 (likewise);
 - the producer/consumer sweep (four consumers per block, forced at this size) against the
   one-lane sweep: bitwise identical temperatures, spectra and dtaus;
 - the species contraction (K3) against the per-species sum in the sweep: within the
@@ -40,7 +42,7 @@ def _run(eng, w, n=6):
 
 def test_full_size_properties(monkeypatch):
     runs = {}
-    variants = (("default", {}), ("again", {}),
+    variants = (("default", {}), ("again", {}), ("one_lane", {"FREI_LAM2": "0"}),
                 ("pair", {"FREI_GROUP_Q": "2", "FREI_SHARED_MAX_BLOCKS": "100000"}),
                 ("pipe", {"FREI_PIPE": "4", "FREI_SHARED_MAX_BLOCKS": "100000"}),
                 ("per_species", {"FREI_PRECONTRACT": "0"}))
@@ -50,6 +52,10 @@ def test_full_size_properties(monkeypatch):
             path = eng.path()
             if name == "pair":
                 assert path["paired"]
+            if name == "default":
+                assert path["lam2"]
+            if name == "one_lane":
+                assert not path["lam2"] and not path["paired"] and path["pipe"] == 0
             if name == "pipe":
                 assert path["pipe"] == 4
             if name == "per_species":
@@ -65,10 +71,12 @@ def test_full_size_properties(monkeypatch):
     assert np.array_equal(a["dtaus"], b["dtaus"])
     assert np.isfinite(a["spectrum"]).all() and (a["spectrum"] > 0).all()
     assert np.isfinite(a["dtaus"]).all()
+    one = runs["one_lane"]
     for k in ("final_T", "spectrum", "dtaus"):
-        assert np.array_equal(runs["pipe"][k], a[k]), k
-    assert rel(runs["pair"]["final_T"], a["final_T"]) < 1e-12
-    assert rel(runs["pair"]["spectrum"], a["spectrum"]) < 1e-9
+        assert np.array_equal(runs["pipe"][k], one[k]), k
+    for v in ("default", "pair"):
+        assert rel(runs[v]["final_T"], one["final_T"]) < 1e-12, v
+        assert rel(runs[v]["spectrum"], one["spectrum"]) < 1e-9, v
     assert rel(runs["per_species"]["final_T"], a["final_T"]) < 1e-10
     # the T-P loop moved the temperatures (6 iterations from the initial profile)
     assert rel(a["final_T"], w_T0()) > 1e-6
