@@ -30,6 +30,17 @@ sys.path.insert(0, ROOT)
 PEAK_HBM = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
 
 
+
+def sweep_kernel_name(path):
+    """The sweep kernel the tables' path selects (frei_ctx_path bits, engine.path())."""
+    if path.get("pipe"):
+        return "sweep_pipe_kernel"
+    if path.get("paired") or path.get("quad"):
+        return "sweep_group_kernel"
+    if path.get("lam2"):
+        return "sweep_pair_kernel"
+    return "sweep_fast_kernel"
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -529,7 +540,7 @@ def main():
             "ms_per_step": el_ps / a.per_species_steps * 1e3, "steps": a.per_species_steps,
             "path": p2,
             "roofline": {"bound": "hbm", "achieved": ach_ps / 1e9, "peak": PEAK_HBM / 1e9,
-                         "unit": "GB/s", "frac": ach_ps / PEAK_HBM, "kernel": "sweep_fast_kernel",
+                         "unit": "GB/s", "frac": ach_ps / PEAK_HBM, "kernel": sweep_kernel_name(p2),
                          "bytes_per_update": bpu_ps, "avg_launch_ms": ps_ms, "launches": ps_n},
             "byte_model": f"8 stale opposite-stream read + 8 live flux write + 16*S = {bpu_ps} B "
                           f"(SURVEY 8(d)'s 24 + 16*S = {24 + 16 * S} B less the dead store the "
@@ -667,7 +678,7 @@ def main():
                          if valu else None,
                          "valu_source": "profiles/valu_sweep.json (SQ_ACTIVE_INST_VALU)"
                          if valu else None,
-                         "kernel": "sweep_fast_kernel", "bytes_per_update": bpu,
+                         "kernel": sweep_kernel_name(path), "bytes_per_update": bpu,
                          "bytes_per_launch": bytes_launch,
                          "avg_launch_ms": avg_sweep_ms, "launches": n_sweeps,
                          "byte_model": (f"contracted table (K3): 8 stale opposite-stream read + "
