@@ -1066,10 +1066,14 @@ __device__ __forceinline__ void sweep_fast_body(
   ring_fence();
   for (int k0 = 0; k0 < ns; k0 += PF) {
 #if FREI_PRIO_PROGRESS
-    // issue priority by progress (diagnostic A/B): a wave early in its layer loop outranks one
-    // near its end, so waves that started late (second-round blocks) catch up instead of
-    // trailing alone at the end of the launch (the hardware otherwise favours the oldest wave)
-    switch ((4 * k0) / ns) {
+    // issue priority by progress (FREI_PRIO_PROGRESS 1): a wave early in its layer loop outranks
+    // one near its end, so waves that started late (second-round blocks) catch up instead of
+    // trailing alone at the end of the launch (the hardware otherwise favours the oldest wave);
+    // 2: a rotating priority (trip + block index) — no wave wins every arbitration; 3: steps
+    // at 1/2, 3/4, 7/8 of the loop (A/B)
+    switch (FREI_PRIO_PROGRESS == 2   ? ((k0 >> 1) + bx) & 3
+            : FREI_PRIO_PROGRESS == 3 ? (2 * k0 < ns ? 0 : 4 * k0 < 3 * ns ? 1 : 8 * k0 < 7 * ns ? 2 : 3)
+                                      : (4 * k0) / ns) {
       case 0: __builtin_amdgcn_s_setprio(3); break;
       case 1: __builtin_amdgcn_s_setprio(2); break;
       case 2: __builtin_amdgcn_s_setprio(1); break;
@@ -1546,7 +1550,9 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
   double* tile = red + (int64_t)(kBlock / 64) * ns * 4;
   for (int k0 = 0; k0 < ns; k0 += 2) {
 #if FREI_PRIO_PROGRESS
-    switch ((4 * k0) / ns) {
+    switch (FREI_PRIO_PROGRESS == 2   ? ((k0 >> 1) + bx) & 3
+            : FREI_PRIO_PROGRESS == 3 ? (2 * k0 < ns ? 0 : 4 * k0 < 3 * ns ? 1 : 8 * k0 < 7 * ns ? 2 : 3)
+                                      : (4 * k0) / ns) {
       case 0: __builtin_amdgcn_s_setprio(3); break;
       case 1: __builtin_amdgcn_s_setprio(2); break;
       case 2: __builtin_amdgcn_s_setprio(1); break;

@@ -70,6 +70,7 @@ def _same(a, b, what):
     ("contracted", {}),
     ("contracted", {"group_q": 1}),
     ("contracted", {"group_q": 2}),
+    ("contracted", {"group_q": 1, "shared": 0, "lam2": 1}),   # two wavelengths per lane
     ("per_species", {"precontract": 0}),
     ("mixed_T", {}),
     ("offnode_p", {}),
@@ -91,6 +92,7 @@ def test_fused_update_is_bitwise_identical_to_two_kernels(fa, name, opts):
         eng.close()
     if name == "contracted":
         assert path["contracted"]
+        assert path["lam2"] == bool(opts.get("lam2", 0))
     if name in ("per_species", "chemistry"):
         assert not path["contracted"]
     a, b = out[1], out[0]
@@ -106,7 +108,8 @@ def test_fused_update_is_bitwise_identical_to_two_kernels(fa, name, opts):
 
 
 @pytest.mark.parametrize("name,opts", [("contracted", {}), ("per_species", {"precontract": 0}),
-                                       ("contracted", {"group_q": 2})])
+                                       ("contracted", {"group_q": 2}),
+                                       ("contracted", {"group_q": 1, "shared": 0, "lam2": 1})])
 def test_graph_replay_is_bitwise_identical_to_launches(fa, name, opts):
     """T-P iterations replayed from a captured hipGraph (frei_iterate / frei_run) against
     kernel-by-kernel launches: same kernels, same arguments, so bit-identical state; the graph

@@ -21,7 +21,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KIND = {1: "sweep_fast", 12: "sweep_group2", 14: "sweep_group4", 21: "sweep_pipe1",
+KIND = {1: "sweep_fast", 2: "sweep_pair", 12: "sweep_group2", 14: "sweep_group4", 21: "sweep_pipe1",
         22: "sweep_pipe2", 24: "sweep_pipe4", 30: "update_fused", 42: "chain_group2",
         44: "chain_group4", 41: "chain_fast", 54: "chain_pipe4"}
 
