@@ -383,6 +383,22 @@ __host__ __device__ inline size_t update_lds_bytes(int nL, int ntn, int S, bool 
   return b;
 }
 
+// Per-block partial sums of a sweep, [blocks][steps x 4] (FREI_PART_BLOCK_MAJOR 1: each block
+// writes its ns x 4 values as whole cache lines; an update workgroup reads its layer's 8 values
+// of every block, one 64-byte span each) or [steps x 4][blocks] (0: the round-1..3 layout).
+#ifndef FREI_PART_BLOCK_MAJOR
+#define FREI_PART_BLOCK_MAJOR 1
+#endif
+__host__ __device__ inline int64_t part_at(int idx, int bx, int nbx, int ns4) {
+#if FREI_PART_BLOCK_MAJOR
+  (void)nbx;
+  return (int64_t)bx * ns4 + idx;
+#else
+  (void)ns4;
+  return (int64_t)idx * nbx + bx;
+#endif
+}
+
 // launchers (frei_kernels.hip)
 void launch_sweep(int dir, const SweepArgs& a, int nblocks, bool fast, hipStream_t st);
 void launch_sweep_fast(int dir, int S, int depth, int pf, bool nan_check, bool shared,

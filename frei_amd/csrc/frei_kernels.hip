@@ -390,7 +390,7 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
   for (int idx = tid; idx < ns * 4; idx += kBlock) {
     double v = red[idx];
     for (int w = 1; w < nw; ++w) v += red[(int64_t)w * ns * 4 + idx];
-    a.part[(int64_t)idx * gridDim.x + blockIdx.x] = v;
+    a.part[part_at(idx, blockIdx.x, gridDim.x, ns * 4)] = v;
   }
 }
 
@@ -1138,7 +1138,7 @@ __device__ __forceinline__ void sweep_fast_body(
     double s = red[idx];
     for (int w = 1; w < red_rows_per_block(a.red_rows); ++w)
       s += red[(int64_t)w * ns * 4 + idx];
-    part[(int64_t)idx * nbx + bx] = s;
+    part[part_at(idx, bx, nbx, ns * 4)] = s;
   }
   TRACE_PUT(CH ? 41 : 1);
 }
@@ -1458,7 +1458,7 @@ __device__ __forceinline__ void sweep_group_body(
     double s = red[idx];
     for (int w = 1; w < red_rows_per_block(a.red_rows, NW); ++w)
       s += red[(int64_t)w * ns * 4 + idx];
-    part[(int64_t)idx * nbx + bx] = s;
+    part[part_at(idx, bx, nbx, ns * 4)] = s;
   }
   TRACE_PUT(CH ? 40 + Q : 10 + Q);
 }
@@ -1653,7 +1653,7 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
   for (int idx = tid; idx < ns * 4; idx += kBlock) {
     double sum = red[idx];
     for (int w = 1; w < kBlock / 64; ++w) sum += red[(int64_t)w * ns * 4 + idx];
-    part[(int64_t)idx * nbx + bx] = sum;
+    part[part_at(idx, bx, nbx, ns * 4)] = sum;
   }
   TRACE_PUT(2);
 }
@@ -2067,7 +2067,7 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
   for (int idx = tid; idx < ns * 4; idx += 256 * NC) {
     double s = red[idx];
     for (int w = 1; w < NC; ++w) s += red[(int64_t)w * ns * 4 + idx];
-    part[(int64_t)idx * nbx + bx] = s;
+    part[part_at(idx, bx, nbx, ns * 4)] = s;
   }
   TRACE_PUT(CH ? 50 + NC : 20 + NC);
 }
@@ -2228,9 +2228,10 @@ __global__ __launch_bounds__(kRedThreads) void reduce_kernel(const double* __res
   conv += blockIdx.y;
   if (!force && *conv) return;
   __shared__ double sh[kRedWaves];
-  const double* p = part + (int64_t)blockIdx.x * nblocks;
+  const int ns4 = gridDim.x;   // one reduce block per (step, quantity)
   double acc = 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += kRedThreads) acc += p[b];
+  for (int b = threadIdx.x; b < nblocks; b += kRedThreads)
+    acc += part[part_at(blockIdx.x, b, nblocks, ns4)];
   // fixed-order butterfly inside each wave, then the wave sums in order: deterministic
   acc = butterfly_sum(acc, threadIdx.x & 63);   // = the xor-32 ... 1 shfl butterfly
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
@@ -2701,8 +2702,10 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
     const double* pj[8];
     for (int j = 0; j < 8; ++j) {
       const int k = (j < 4) ? (k0 >= 0 ? k0 : k1) : (k1 >= 0 ? k1 : k0);
-      pj[j] = a.part + (int64_t)(k * 4 + (j & 3)) * a.nblocks;
+      pj[j] = a.part + part_at(k * 4 + (j & 3), 0, a.nblocks, 4 * (nL - 1));
     }
+    // element of block b in row j: pj[j][b * bs]
+    const int64_t bs = part_at(0, 1, a.nblocks, 4 * (nL - 1));
     double acc[8];
     for (int j = 0; j < 8; ++j) acc[j] = 0.0;
     // U strided partials of all 8 rows loaded before any is added (one round trip per batch,
@@ -2715,7 +2718,7 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
     if constexpr (U == 1) {
 #pragma unroll 2
       for (int b = tid; b < nb; b += kRedThreads)
-        for (int j = 0; j < 8; ++j) acc[j] += pj[j][b];
+        for (int j = 0; j < 8; ++j) acc[j] += pj[j][b * bs];
     } else
     for (int b0 = tid; b0 < nb; b0 += kU * kRedThreads) {
       double v[kU][8];
@@ -2723,7 +2726,7 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
       for (int u = 0; u < kU; ++u) {
         const int b = min(b0 + u * kRedThreads, nb - 1);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[u][j] = pj[j][b];
+        for (int j = 0; j < 8; ++j) v[u][j] = pj[j][b * bs];
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u)
