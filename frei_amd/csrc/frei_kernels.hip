@@ -1560,8 +1560,11 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
     }
 #endif
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {   // step k0 + 1 past the end: a dummy, computed, not stored
+    for (int g = 0; g < 2; ++g) {
       const int k = k0 + g;
+      // odd step counts: no work past the last step (the pair's reduction below then reads a
+      // stale tile slot for it and writes nothing for it)
+      if (k >= ns) break;
       const int kk = clampk(k);
       ring_fence();
       const FastStep& sk = st[kk];
