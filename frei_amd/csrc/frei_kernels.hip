@@ -594,46 +594,15 @@ __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, dou
   c.dtau = dtau;
 }
 
-// General step (twostream.py:139-176): E of Deitrick 2020 Eqn 19 where w0 > 0.1, else 1.
-template <bool NF = false>
-__device__ __forceinline__ void coef_from(double w0, double dtau, double B1, double B2,
-                                          StepCoef& c) {
-  const double E = (w0 > 0.1) ? ((1.225 - 0.1777 * w0) - 0.05582 * (w0 * w0)) : 1.0;
-  const double Emw = E - w0;
-  const double q = fm::div(fm::div(B1 - B2, dtau), 2.0 * E);
-  // E = 1 lanes take pi like coef_e1, so both forms give the same bits on them
-#if FREI_PI_E1 || FREI_LEAN
-  const double pi_w = (w0 > 0.1) ? fm::div(kPi * (1.0 - w0), Emw) : kPi;
-#else
-  const double pi_w = fm::div(kPi * (1.0 - w0), Emw);
-#endif
-  coef_tail<NF>(w0, dtau, B1, B2, fm::sqrt_pos(E * Emw), fm::sqrt_pos(fm::div(Emw, E)), q,
-                pi_w, c);
-}
-
-// Step whose w0 <= 0.1 (E = 1): E * Emw, Emw / E and Bprime / (2 E) are exact without the
-// multiply/divide and sqrt(E * Emw) == sqrt(Emw / E), so this skips two divisions and a
-// square root with bit-identical results.  pi (1 - w0) / (1 - w0) is pi within an ulp (the
-// reference's own rounding of it), so the constant replaces a third division.  Taken when
-// the whole wave qualifies.
-template <bool NF = false>
-__device__ __forceinline__ void coef_e1(double w0, double dtau, double B1, double B2,
-                                        StepCoef& c) {
-  const double Emw = 1.0 - w0;
-  const double sq = fm::sqrt_pos(Emw);
-#if FREI_PI_E1 || FREI_LEAN
-  coef_tail<NF>(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5, kPi, c);
-#else
-  coef_tail<NF>(w0, dtau, B1, B2, sq, sq, fm::div(B1 - B2, dtau) * 0.5,
-                fm::div(kPi * (1.0 - w0), Emw), c);
-#endif
-}
-
-// The E-dependent head of a step's coefficients (sq = sqrt(E (E - w0)), r = sqrt((E - w0) / E),
-// q = B' / 2E, pi_w) ahead of the shared coef_tail: the E = 1 values for every lane, then — in a
-// wave-uniform branch taken only when some lane has w0 > 0.1 — coef_from's values on those
-// lanes.  The same bits as coef_e1 / coef_from on every lane, with ONE tail in the loop: the
-// tail duplicated in both branches had set the sweep's register budget (12 VGPRs).
+// The E-dependent head of a step's coefficients (twostream.py:139-176; E of Deitrick 2020
+// Eqn 19 where w0 > 0.1, else 1): sq = sqrt(E (E - w0)), r = sqrt((E - w0) / E), q = B' / 2E and
+// pi_w, ahead of the shared coef_tail.  Every lane first takes the E = 1 values — there E Emw,
+// Emw / E and B' / 2E are exact without the multiply / divide and sqrt(E Emw) == sqrt(Emw / E)
+// (bit-identical, two divisions and a square root fewer), and pi (1 - w0) / (1 - w0) is pi
+// within an ulp (the reference's own rounding of it).  Only when some lane of the wave has
+// w0 > 0.1 does a wave-uniform branch patch those lanes with the general E (coef_head_general).
+// One tail in the loop instead of one per branch: the duplicated tail had set the sweep's
+// register budget (4 VGPRs).
 struct CoefHead {
   double sq, r, q, pi_w;
 };
