@@ -1,0 +1,19 @@
+#!/bin/bash
+# Update partial sums in 8-lane groups (l8: whole-span loads of the block-major partials) vs the
+# per-thread strided form (base), interleaved at 500k and at the 8-GPU slice; then the update /
+# chain / multirank / batch tests and the in-kernel traces.
+set -o pipefail
+O=gpurun_out/${1:-r04l8}
+mkdir -p $O
+B="--no-cpu-baseline --no-binning --no-c5 --no-chemistry --no-per-species --steps 20 --warmup 5"
+for rep in 1 2 3; do
+  for t in l8 base; do
+    E="FREI_HIP_LIB=ablib/$t.so"
+    env $E timeout -k 10 120 python3 bench.py $B > $O/${t}_500k_$rep.json 2> /dev/null || { echo "bench $t failed"; exit 3; }
+    env $E timeout -k 10 120 python3 bench.py $B --rad-eq-max 1 --steps 40 --force-comm --lam-slice 0:62500 > $O/${t}_s8_$rep.json 2> /dev/null || { echo "bench s8 $t failed"; exit 3; }
+    python3 -c "import json; a=json.load(open('$O/${t}_500k_$rep.json')); c=json.load(open('$O/${t}_s8_$rep.json')); print('$t', $rep, '500k %.4f ms' % a['ms_per_step'], '62.5k %.2f us' % (c['ms_per_step']*1e3), flush=True)" | tee -a $O/summary.txt
+  done
+done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fused_update.py tests/test_gpu_chain.py tests/test_gpu_multirank.py tests/test_gpu_batch.py tests/test_gpu_lam2.py -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+grep -E "FAILED|ERROR" $O/pytest.log | head; tail -1 $O/pytest.log
+bash tools/r04_trace2.sh ${1:-r04l8}/trace
