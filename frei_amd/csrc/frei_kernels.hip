@@ -1039,8 +1039,9 @@ __device__ __forceinline__ void sweep_fast_body(
     // one near its end, so waves that started late (second-round blocks) catch up instead of
     // trailing alone at the end of the launch (the hardware otherwise favours the oldest wave);
     // 2: a rotating priority (trip + block index) — no wave wins every arbitration; 3: steps
-    // at 1/2, 3/4, 7/8 of the loop (A/B)
+    // at 1/2, 3/4, 7/8 of the loop; 4: rotating with the block's dispatch round (A/B)
     switch (FREI_PRIO_PROGRESS == 2   ? ((k0 >> 1) + bx) & 3
+            : FREI_PRIO_PROGRESS == 4 ? ((k0 >> 1) + (bx >> 8)) & 3
             : FREI_PRIO_PROGRESS == 3 ? (2 * k0 < ns ? 0 : 4 * k0 < 3 * ns ? 1 : 8 * k0 < 7 * ns ? 2 : 3)
                                       : (4 * k0) / ns) {
       case 0: __builtin_amdgcn_s_setprio(3); break;
@@ -1520,6 +1521,7 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
   for (int k0 = 0; k0 < ns; k0 += 2) {
 #if FREI_PRIO_PROGRESS
     switch (FREI_PRIO_PROGRESS == 2   ? ((k0 >> 1) + bx) & 3
+            : FREI_PRIO_PROGRESS == 4 ? ((k0 >> 1) + (bx >> 8)) & 3
             : FREI_PRIO_PROGRESS == 3 ? (2 * k0 < ns ? 0 : 4 * k0 < 3 * ns ? 1 : 8 * k0 < 7 * ns ? 2 : 3)
                                       : (4 * k0) / ns) {
       case 0: __builtin_amdgcn_s_setprio(3); break;
