@@ -298,6 +298,13 @@ int h2d(T* d, const T* h, size_t n, hipStream_t st) {
 
 // Species contraction (K3) when every species shares its nodes (one bracket per layer), no
 // table holds a NaN (the reference's nansum, Q8, is per species) and S >= 2.
+// two wavelengths per lane from this many one-lane blocks per launch (all atmospheres of a
+// batched launch): about 1.1 rounds of the one-lane form at five waves per SIMD
+constexpr int kLam2MinBlocks = 1400;
+bool lam2_blocks(const frei_ctx* c) {
+  return (int64_t)c->nblocks * (c->n_atm > 1 ? c->n_atm : 1) >= kLam2MinBlocks;
+}
+
 template <typename Lap>
 int build_contracted(frei_ctx* c, bool shared_fast, Lap&& lap) {
   const int nL = c->nL, S = c->S;
@@ -503,7 +510,10 @@ int build_meta(frei_ctx* c) {
     shared = shared && q.n_p == q0.n_p && q.n_T == q0.n_T && q.stride == q0.stride &&
              q.p_nodes == q0.p_nodes && q.T_nodes == q0.T_nodes;
   }
-  const bool small = c->nblocks <= c->shared_max_blocks;
+  // batched launches with many blocks in all take the two-wavelength sweep, which reads the
+  // step records from global memory (C5, 32 x 100k lambda: -9 % per step, profiles/r04/c5/)
+  const bool lam2_batch = c->n_atm > 1 && c->lam2 != 0 && c->nlam % 2 == 0 && lam2_blocks(c);
+  const bool small = c->nblocks <= c->shared_max_blocks && !lam2_batch;
   // the LDS-staged step table plus one partial-sum row per wave must leave room for several
   // blocks per CU (deep atmospheres: > ~260 layers read the step table from global memory)
   const size_t ns_l = (size_t)nL - 1;
@@ -565,10 +575,6 @@ SetupArgs setup_args(frei_ctx* c);
 // Sweeps form their own step records in their prologue (and the update kernels skip writing
 // them) when the sweep reads the shared-bracket records from LDS — every form on the contracted
 // table with shared brackets — and the mixing ratios are fixed (no T-dependent chemistry).
-// two wavelengths per lane from this many one-lane blocks (about 1.1 rounds of the one-lane
-// form at five waves per SIMD)
-constexpr int kLam2MinBlocks = 1400;
-
 bool records_in_sweep(frei_ctx* c) {
   if (!(c->rec_sweep && c->fast && c->eff && c->shared && !c->chem_on)) return false;
   // auto: not for batched contexts (every (block, atmosphere) would form the records: C5 -2 %,
@@ -817,7 +823,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
     // about one round of one-lane blocks (1280 resident at five waves per SIMD on 256 CUs)
     const bool lam2 = c->lam2 != 0 && c->eff && S_run == 1 && !c->shared && !nan_check &&
                       Q == 1 && NC == 0 && !merge && depth == 2 && pf <= 2 && f.red_rows == 2 &&
-                      c->nlam % 2 == 0 && (c->lam2 > 0 || c->nblocks >= kLam2MinBlocks);
+                      c->nlam % 2 == 0 && (c->lam2 > 0 || lam2_blocks(c));
     if (lam2) nb_run = (int)((c->nlam + 2 * kBlock - 1) / (2 * kBlock));
     if (c->keys) {
       uint64_t h = arg_hash(1469598103934665603ull, f);
@@ -2122,7 +2128,7 @@ int frei_ctx_path(frei_ctx* c, int* flags) {
   const int NC = pipe_consumers(c);
   // (the sweep itself also requires a depth-2 coefficient block with staged sums: the defaults)
   const bool lam2 = c->lam2 != 0 && c->fast && c->eff && !c->shared && Q == 1 && NC == 0 &&
-                    c->nlam % 2 == 0 && (c->lam2 > 0 || c->nblocks >= kLam2MinBlocks) &&
+                    c->nlam % 2 == 0 && (c->lam2 > 0 || lam2_blocks(c)) &&
                     c->prefetch_depth != 1 && c->prefetch_depth < 4 && c->prefetch_steps <= 2 &&
                     c->red_stage;
   *flags = (c->fast ? 1 : 0) | (c->fast && c->shared ? 2 : 0) | (c->eff ? 4 : 0) |
