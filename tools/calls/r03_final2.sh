@@ -4,4 +4,4 @@ set -e -o pipefail
 O=gpurun_out/${1:-final2}
 mkdir -p $O
 timeout -k 10 300 ./tools/mathcheck > $O/mathcheck.txt 2>&1; cat $O/mathcheck.txt
-bash tools/r03_verify.sh ${1:-final2}
+bash tools/calls/r03_verify.sh ${1:-final2}

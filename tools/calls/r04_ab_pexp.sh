@@ -22,6 +22,6 @@ for rep in 1 2 3; do
     python3 -c "import json; a=json.load(open('$O/${t}_500k_$rep.json')); b=json.load(open('$O/${t}_s0_$rep.json')); print('$t', $rep, '500k %.4f ms sweep %.2f us' % (a['ms_per_step'], a['roofline']['avg_launch_ms']*1e3), 'slice0 %.2f us' % (b['ms_per_step']*1e3), flush=True)" | tee -a $O/summary.txt
   done
 done
-bash tools/r04_rounds.sh ${1:-r04pexp}/rounds
+bash tools/calls/r04_rounds.sh ${1:-r04pexp}/rounds
 FREI_PARITY_JSON=$O/parity.json timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 700 --timeout-method thread > $O/pytest.log 2>&1
 grep -E "FAILED" $O/pytest.log | head -20; tail -1 $O/pytest.log

@@ -17,4 +17,4 @@ for rep in 1 2 3; do
     python3 -c "import json; a=json.load(open('$O/${t}_500k_$rep.json')); print('$t', $rep, '500k %.4f ms sweep %.2f us' % (a['ms_per_step'], a['roofline']['avg_launch_ms']*1e3), flush=True)" | tee -a $O/summary.txt
   done
 done
-bash tools/r04_rounds.sh ${1:-r04c8}/rounds
+bash tools/calls/r04_rounds.sh ${1:-r04c8}/rounds

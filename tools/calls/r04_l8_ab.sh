@@ -16,4 +16,4 @@ for rep in 1 2 3; do
 done
 timeout -k 10 600 python -u -m pytest tests/test_gpu_fused_update.py tests/test_gpu_chain.py tests/test_gpu_multirank.py tests/test_gpu_batch.py tests/test_gpu_lam2.py -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 grep -E "FAILED|ERROR" $O/pytest.log | head; tail -1 $O/pytest.log
-bash tools/r04_trace2.sh ${1:-r04l8}/trace
+bash tools/calls/r04_trace2.sh ${1:-r04l8}/trace
