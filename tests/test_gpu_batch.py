@@ -244,3 +244,33 @@ def test_batched_step_records_formed_in_sweep_are_bitwise_the_updates(fa, monkey
     assert np.array_equal(a["final_T"], b["final_T"])
     assert np.array_equal(a["spectra"], b["spectra"])
     assert all(np.array_equal(x, y) for x, y in zip(fa_, fb_))
+
+
+def test_batched_two_wavelength_sweep_matches_one_lane(fa, monkeypatch):
+    """Two wavelengths per lane over (wavelength block, atmosphere) launches (forced here; the
+    C5 size selects it by itself, test_gpu_c5_fullsize.py): every atmosphere's single-sweep
+    fluxes are the one-lane sweep's bit for bit, so after a run the temperatures differ only by
+    the bolometric summation tree, with equal iteration counts.  That difference is rounding,
+    but the deepest layer's dT amplifies it: 2e-11 relative after six iterations here, so the
+    bound is the parity bar (1e-10; the oracle pins this form at C5 size in
+    test_gpu_c5_fullsize.py)."""
+    names = ["1H2-16O", "12C-16O", "Na"]
+    lam, p, tabs_o, tabs_f, g, mmr, T0 = _setup(fa, 3, 3000, 24, names, 23)
+    out = {}
+    monkeypatch.setenv("FREI_GROUP_Q", "1")
+    monkeypatch.setenv("FREI_PIPE", "0")
+    monkeypatch.setenv("FREI_SHARED", "0")
+    for v in (0, 1):
+        monkeypatch.setenv("FREI_LAM2", str(v))
+        eng = fa.BatchEngine(lam, p, tabs_f, g=g, mmr=mmr)
+        try:
+            path = eng.path()
+            assert path["contracted"] and path["lam2"] == bool(v), path
+            r = eng.run(T0, n_timesteps=6, n_zero_crossings=10 ** 6, convergence_dT=-1.0)
+            out[v] = (r, eng.get_fluxes())
+        finally:
+            eng.close()
+    (r0, _), (r1, _) = out[0], out[1]
+    assert np.array_equal(r0["n_iter"], r1["n_iter"])
+    assert rel(r1["final_T"], r0["final_T"]) < 1e-10
+    assert row_normwise(r1["spectra"], r0["spectra"]) < 1e-9
