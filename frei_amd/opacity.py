@@ -8,7 +8,7 @@ DataArray).  ``kappa`` evaluates on the GPU through the C ABI (frei_kappa).
 import numpy as np
 
 from .constants import M_BAR_DEFAULT, UM
-from .units import scalar, value
+from .units import scalar, unit_of, value, with_unit
 
 __all__ = ["OpacityTable", "SeparableTable", "kappa", "load_example_opacity",
            "rayleigh_H2", "rayleigh_He", "binned_opacity"]
@@ -163,13 +163,17 @@ def kappa(opacities, temperature, pressure, lam, m_bar=M_BAR_DEFAULT, device=0,
                         device=device, tag=None if chemistry is None else ("kappa", id(chemistry)))
     names = list(opacities)
 
+    # Quantities in -> (k, sigma) in cm^2 g^-1 Quantities out (opacity.py:269)
+    ku = unit_of("cm2 / g", temperature, pressure, lam, m_bar)
+
     def query(Tq, pq):
         if chemistry is not None:
             m = provider_mmr(chemistry, [Tq], [pq], names, mb)[:, 0]
             eng.set_mmr(np.repeat(m[:, None], _KAPPA_P.size, axis=1))
         return eng.kappa(Tq, pq)
     if T.ndim == 0 and p.ndim == 0:
-        return query(float(T), float(p))
+        k, sig = query(float(T), float(p))
+        return with_unit(k, ku), with_unit(sig, ku)
     # vector mode: points along one dimension z (opacity.py:235-263).  The reference
     # flattens the (z, lam) result before adding sigma (opacity.py:266-269), so a one-point
     # array gives a flat k; for z > 1 its broadcast fails, and here k is (z, lam).
@@ -179,9 +183,8 @@ def kappa(opacities, temperature, pressure, lam, m_bar=M_BAR_DEFAULT, device=0,
     for Tq, pq in zip(Tz.ravel(), pz.ravel()):
         k, sig = query(float(Tq), float(pq))
         ks.append(k)
-    if len(ks) == 1:
-        return ks[0], sig
-    return np.array(ks).reshape(Tz.shape + (lam_um.size,)), sig
+    k = ks[0] if len(ks) == 1 else np.array(ks).reshape(Tz.shape + (lam_um.size,))
+    return with_unit(k, ku), with_unit(sig, ku)
 
 
 def load_example_opacity(grid, seed=42, scale_factor=20):

@@ -3,13 +3,16 @@
 Same names, arguments and tuple returns as the reference; ``fluxes_up``/``fluxes_down``
 passed by the caller are updated in place and returned (twostream.py:290-294, 418-421).
 Units: wavelength µm, temperature K, pressure bar, flux erg s^-1 cm^-3, g cm s^-2,
-m_bar g (astropy Quantities are accepted and converted when astropy is installed).
+m_bar g.  Quantities are accepted and converted; when the caller passes Quantities, the
+results come back as Quantities in those units (frei_amd/units.py).
 """
 import numpy as np
 
 from .constants import C, H, K_B, M_BAR_DEFAULT, UM
 from .engine import ABSORB, EMIT, cached_engine, propagate_fluxes_device
-from .units import scalar, value
+from .units import assign, scalar, unit_of, value, with_unit
+
+FLUX = "erg / (s cm3)"
 
 __all__ = ["propagate_fluxes", "emit", "absorb", "BB", "E"]
 
@@ -37,12 +40,13 @@ def propagate_fluxes(lam, F_1_up, F_2_down, T_1, T_2, delta_tau, omega_0=0, g_0=
     (twostream.py:97-177) -> (F_2_up, F_1_down).  ``g_0`` (scalar or per wavelength) enters
     E, the transmission, zeta and B' through (1 - omega_0 g_0) as in the reference; emit and
     absorb use g_0 = 0 (twostream.py:389, 518).  ``eps`` is unused as in the reference."""
-    flux = "erg / (s cm3)"
-    return propagate_fluxes_device(value(lam, "um"), value(F_1_up, flux), value(F_2_down, flux),
-                                   scalar(T_1, "K"), scalar(T_2, "K"),
-                                   np.asarray(delta_tau, dtype=float),
-                                   np.asarray(omega_0, dtype=float),
-                                   g_0=np.asarray(g_0, dtype=float), device=device)
+    up, down = propagate_fluxes_device(value(lam, "um"), value(F_1_up, FLUX),
+                                       value(F_2_down, FLUX), scalar(T_1, "K"), scalar(T_2, "K"),
+                                       np.asarray(delta_tau, dtype=float),
+                                       np.asarray(omega_0, dtype=float),
+                                       g_0=np.asarray(g_0, dtype=float), device=device)
+    flux_u = unit_of(FLUX, F_1_up, F_2_down, lam, T_1)     # Quantities in -> Quantities out
+    return with_unit(up, flux_u), with_unit(down, flux_u)
 
 
 def _sweeps(direction, opacities, temperatures, pressures, lam, F_TOA, g, m_bar, n_timesteps,
@@ -51,16 +55,15 @@ def _sweeps(direction, opacities, temperatures, pressures, lam, F_TOA, g, m_bar,
     p = np.asarray(value(pressures, "bar"), dtype=float)
     lam_um = np.asarray(value(lam, "um"), dtype=float)
     nL, nlam = p.size, lam_um.size
-    ftoa = np.asarray(value(F_TOA, "erg / (s cm3)"), dtype=float)
+    ftoa = np.asarray(value(F_TOA, FLUX), dtype=float)
     thresh = scalar(convergence_thresh, "K")
     # the context (uploaded tables) is reused by later calls with the same opacity dict
     eng = cached_engine(opacities, lam_um=lam_um, p_bar=p, g=scalar(g, "cm / s2"),
                         m_bar=scalar(m_bar, "g"), F_toa=ftoa, device=device,
                         chemistry=chemistry)
     up_in, down_in = fluxes_up, fluxes_down
-    up = np.zeros((nL, nlam)) if up_in is None else np.array(value(up_in, "erg / (s cm3)"))
-    down = (np.zeros((nL, nlam)) if down_in is None
-            else np.array(value(down_in, "erg / (s cm3)")))
+    up = np.zeros((nL, nlam)) if up_in is None else np.array(value(up_in, FLUX))
+    down = np.zeros((nL, nlam)) if down_in is None else np.array(value(down_in, FLUX))
     if up_in is None and direction == ABSORB:
         up[0] = np.pi * BB(T[0])(lam_um)          # twostream.py:468-470 (Q5)
     if down_in is None:
@@ -78,14 +81,15 @@ def _sweeps(direction, opacities, temperatures, pressures, lam, F_TOA, g, m_bar,
         if n_timesteps > 1 and np.abs(dT).max() < thresh:
             break
     up, down = eng.get_fluxes()
-    # the reference mutates the caller's arrays in place
-    if isinstance(up_in, np.ndarray) and up_in.dtype == np.float64:
-        up_in[...] = up
-        up = up_in
-    if isinstance(down_in, np.ndarray) and down_in.dtype == np.float64:
-        down_in[...] = down
-        down = down_in
-    return up, down, hist[:, j + 1].copy(), hist, dtaus, dT
+    # the reference mutates the caller's arrays in place (Quantities through their own unit)
+    # and returns them; fluxes it allocated itself carry erg s^-1 cm^-3, temperatures K, and
+    # dtaus is a plain array (twostream.py:334-339, 418-421, 547-550)
+    flux_u = unit_of(FLUX, up_in, down_in, F_TOA, temperatures, lam)
+    K_u = unit_of("K", temperatures, convergence_thresh, up_in, F_TOA)
+    up = with_unit(up, flux_u) if up_in is None else assign(up_in, up, FLUX)
+    down = with_unit(down, flux_u) if down_in is None else assign(down_in, down, FLUX)
+    return (up, down, with_unit(hist[:, j + 1].copy(), K_u), with_unit(hist, K_u), dtaus,
+            with_unit(dT, K_u))
 
 
 def emit(opacities, temperatures, pressures, lam, F_TOA, g, m_bar=M_BAR_DEFAULT,

@@ -22,22 +22,25 @@ def pytest_runtest_logreport(report):
 
 
 def _provenance(session, exitstatus):
-    """Which tree and run produced a parity log: the git head recorded in .tree_stamp
-    (tools/stamp_tree.sh writes it before a GPU call: the box's snapshot has no .git), the
-    source hash the native library was built from, host, time, the pytest arguments and the
-    session's outcome counts."""
+    """Which tree and run produced a parity log: the hash of the shipped source tree computed
+    from the files on the machine that ran (tests/provenance.py; equal to
+    ``python -m tests.provenance`` on the committed checkout), the source hash the native
+    library was built from, host, time, the pytest arguments and the session's outcome
+    counts."""
     import datetime
     import socket
+    from tests.provenance import tree_hash
+    digest, n_files = tree_hash(ROOT)
     prov = {"host": socket.gethostname(),
             "utc": datetime.datetime.now(datetime.timezone.utc).isoformat(timespec="seconds"),
             "pytest_args": [str(a) for a in session.config.invocation_params.args],
-            "exitstatus": int(exitstatus), "outcomes": dict(_OUTCOMES)}
-    for key, name in (("tree", ".tree_stamp"), ("lib_source_hash", "frei_amd/libfrei_hip.so.stamp")):
-        try:
-            with open(os.path.join(ROOT, name)) as f:
-                prov[key] = f.read().strip()
-        except OSError:
-            prov[key] = None
+            "exitstatus": int(exitstatus), "outcomes": dict(_OUTCOMES),
+            "tree_hash": digest, "tree_files": n_files}
+    try:
+        with open(os.path.join(ROOT, "frei_amd/libfrei_hip.so.stamp")) as f:
+            prov["lib_source_hash"] = f.read().strip()
+    except OSError:
+        prov["lib_source_hash"] = None
     return prov
 
 

@@ -18,6 +18,10 @@ Cases (file -> reference functions exercised):
   c1_step1.npz      Grid.emission_spectrum(n_timesteps=1), example opacity + gray variant (core.py:233-338)
   c1_converge.npz   Grid.emission_spectrum(n_timesteps=100) to convergence
   c2small.npz       60 x 2048, 2 species separable T-varying tables (16 T nodes), 3 iterations
+  c1_vmr3e4.npz     test_core.py:19-71's Grid (example opacity, n_timesteps=1) with kappa's
+                    chemistry a constant VMR of 3e-4 -- the H2O maximum FastChem gives in the
+                    reference's CI (test_chemistry.py:45-46), which reproduces its pins
+                    (test_core.py:51-71)   (opacity.py:246-248, core.py:233-338)
 """
 import os
 import sys
@@ -333,6 +337,38 @@ def case_c2small():
     o, _, _, _ = spectrum_case(g, 3, "")
     out.update(o)
     save("c2small.npz", **out)
+
+
+def vmr_chemistry(vmr):
+    """A chemistry provider on the reference's signature (chemistry.py:114-116) returning a
+    constant volume mixing ratio ``vmr`` for every species: mmr = vmr * mass / m_bar, the
+    mock's formula (chemistry.py:197-199, 243) with another VMR."""
+    def chemistry(temperatures, pressures, species, return_vmr=False, m_bar=None):
+        n = np.atleast_1d(temperatures.value).shape
+        mmr = {iso: np.full(n, vmr) * (R.chemistry.iso_to_mass(iso) / m_bar)
+               .to(u.dimensionless_unscaled).value for iso in species}
+        return (mmr, {iso: np.full(n, vmr) for iso in species}) if return_vmr else mmr
+    return chemistry
+
+
+def case_c1_vmr3e4():
+    pl = planet()
+    g = R.core.Grid(pl, T_ref=2400 * u.K)
+    g.load_opacities(opacities=R.opacity.load_example_opacity(g, scale_factor=1))
+    chem = vmr_chemistry(3e-4)
+    saved = R.opacity.chemistry
+    R.opacity.chemistry = chem            # what kappa calls (opacity.py:11, 246-248)
+    try:
+        out, spec, T, dtaus = spectrum_case(g, 1, "")
+        out["Teff"] = R.core.effective_temperature(g, spec, dtaus, T).to(u.K).value
+    finally:
+        R.opacity.chemistry = saved
+    out["lam"] = g.lam.to(u.um).value
+    out["peak_lam"] = spec.wavelength[spec.flux.argmax()].to(u.um).value
+    out["peak_flux"] = spec.flux.max().to(FLUX).value
+    out["mmr"] = chem(g.init_temperatures, g.pressures, ["1H2-16O"], m_bar=pl.m_bar)["1H2-16O"]
+    save("c1_vmr3e4.npz", **out)
+    print("peak", out["peak_lam"], "um", out["peak_flux"], "Teff", out["Teff"])
 
 
 if __name__ == "__main__":

@@ -51,7 +51,10 @@ def oracle_mmr(provider):
     return f
 
 
-def _case(n_lam=600, nL=30, T_ref=1600.0):
+def _case(n_lam=600, nL=30, T_ref=1600.0, log_lo=-3.0, log_hi=1.0):
+    """Tables 10^U(log_lo, log_hi) cm^2/g x (p/bar)^0.1 x (T/1000 K)^0.5 on 11 T nodes.  The
+    default range leaves the top layers nearly transparent (dtau ~ 1e-7: one ulp of exp moves
+    the spectrum by 2.4e-8); log 1..3 is the well-conditioned case (one-ulp floor ~1e-12)."""
     rng = np.random.default_rng(19)
     lam, _, _ = O.wavelength_grid(0.5, 10, n_lam)
     p = O.pressure_grid(nL, -6, np.log10(200))
@@ -59,7 +62,7 @@ def _case(n_lam=600, nL=30, T_ref=1600.0):
     Tn = np.linspace(0.6 * T0.min(), 1.4 * T0.max(), 11)
     tabs_o, base = {}, {}
     for n in NAMES:
-        base[n] = 10 ** rng.uniform(-3, 1, lam.size)
+        base[n] = 10 ** rng.uniform(log_lo, log_hi, lam.size)
         tabs_o[n] = O.Table(O.separable_table(base[n], (p / 1.0) ** 0.1, (Tn / 1000.0) ** 0.5),
                             p, Tn)
     return lam, p, T0, Tn, base, tabs_o
@@ -115,6 +118,47 @@ def test_grid_feeds_the_provider_to_radiative_equilibrium(fa):
     assert n_calls >= 2 * it + 1
     # the provider's values, not the mock's, reached kappa
     assert rel(mspec.flux, osp) > 1e-3 and rel(mT, oT) > 1e-3
+
+
+class BumpedFastChem(FakeFastChem):
+    """The same provider with CO's mass mixing ratio 1e-8 (relative) higher."""
+
+    def __call__(self, *a, **k):
+        out = super().__call__(*a, **k)
+        out["12C-16O"] = out["12C-16O"] * (1 + 1e-8)
+        return out
+
+
+def test_provider_radiative_equilibrium_at_1e10_outright(fa):
+    """VERDICT r04 "next" #2: the provider path on a well-conditioned atmosphere (opacities
+    10-1000 cm^2/g: the oracle's own one-ulp floor <= 1e-10 on every output), held to 1e-10 with
+    no floor widening — spectrum elementwise, F_up / F_down row-normwise, T, T history and dtaus
+    elementwise, equal iteration counts — and the criterion has teeth: the oracle with one
+    species' mmr moved by 1e-8 is rejected."""
+    lam, p, T0, Tn, base, tabs_o = _case(log_lo=1.0, log_hi=3.0)
+    prov = FakeFastChem()
+    grid = fa.Grid(fa.Planet.from_hot_jupiter(), lam=lam, pressures=p, init_temperatures=T0)
+    grid.load_opacities(opacities=_tabs_f(fa, p, Tn, base), chemistry=prov)
+    spec, T, th, dtaus = grid.emission_spectrum(n_timesteps=60)
+    eng = grid.engine()
+    assert eng.provider is prov and not eng.path()["contracted"]
+    up, down = eng.get_fluxes()
+
+    def run(provider):
+        return O.emission_spectrum(tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1,
+                                   n_timesteps=60, mmr=oracle_mmr(provider))
+    osp, oT, oth, odt, ou, od, it = run(FakeFastChem())
+    with perturbed_exp():
+        psp, pT, pth, pdt, pu, pd, _ = run(FakeFastChem())
+    floor = grid_floor(osp, ou, od, psp, pu, pd)
+    assert max(floor) <= 1e-10 and rel(pT, oT) <= 1e-10 and rel(pdt, odt) <= 1e-10, floor
+    assert th.shape[1] == 2 * it and 2 < it < 60, "iterations to convergence"
+    assert_grid_parity(spec.flux, osp, up, ou, down, od, "chemistry provider, well conditioned",
+                       T=T, ref_T=oT)                       # no floor: 1e-10 outright
+    assert rel(th, oth) <= 1e-10 and rel(dtaus, odt) <= 1e-10, (rel(th, oth), rel(dtaus, odt))
+    bsp, bT, _, _, bu, bd, _ = run(BumpedFastChem())
+    assert max(rel(spec.flux, bsp), rel(T, bT)) > 1e-10    # a 1e-8 mmr error would fail
+    assert rel(bsp, osp) > 1e-9
 
 
 def test_reference_mock_as_provider_keeps_the_device_loop(fa):

@@ -3,12 +3,19 @@
 test_grid_init and test_example_opacities keep the reference's structure and assertions.  The
 reference's numeric checks of the emergent spectrum (peak at 1.1518 µm, peak flux 1.296e13,
 T_eff 2400 ± 200 K) come from its CI run with real FastChem, which is third-party and absent
-here (parity unpinned for FastChem); with the reference's own mock chemistry the reference
-itself gives a peak at lam[198] = 1.641 µm, 6.74e12 erg s^-1 cm^-3 and T_eff 2188.9 K
-(tests/golden/c1_step1.npz, generated by the reference), which the same assertions check here.
+here.  Two runs check them:
+- ``test_core_pins_with_fastchem_vmr``: kappa's chemistry passed through ``chemistry=`` as a
+  constant VMR of 3e-4 — the H2O maximum FastChem gives in the reference's CI
+  (test_chemistry.py:45-46) — asserts the pins literally and matches the reference itself run
+  with that chemistry (tests/golden/c1_vmr3e4.npz) at 1e-10;
+- ``test_example_opacities``: the reference's own mock chemistry (VMR 1.5e-3), for which the
+  reference gives a peak at lam[198] = 1.641 µm, 6.74e12 erg s^-1 cm^-3 and T_eff 2188.9 K
+  (tests/golden/c1_step1.npz).
 """
 import numpy as np
 import pytest
+
+from tests.parity import assert_grid_parity, rel
 
 pytestmark = pytest.mark.gpu
 
@@ -54,3 +61,49 @@ def test_example_opacities(fa, golden):
     teff = fa.effective_temperature(grid, spec, dtaus, temps)
     assert abs(teff - float(C["ex_Teff"])) < 1e-6
     assert abs(teff - T_ref) < 250.0   # the reference's 200 K band, widened for mock chemistry
+
+
+def vmr_provider(vmr):
+    """A chemistry provider on the reference's signature (chemistry.py:114-116): constant VMR,
+    mmr = VMR * mass / m_bar (the mock's formula, chemistry.py:197-199)."""
+    from frei_amd.chemistry import iso_to_mass
+    from frei_amd.constants import AMU
+
+    def chemistry(temperatures, pressures, species, return_vmr=False, m_bar=None):
+        n = np.shape(np.atleast_1d(getattr(temperatures, "value", temperatures)))
+        mb = float(getattr(m_bar, "value", m_bar))
+        return {iso: np.full(n, vmr) * (iso_to_mass(iso) * AMU / mb) for iso in species}
+    return chemistry
+
+
+def test_core_pins_with_fastchem_vmr(fa, golden):
+    """test_core.py:51-71 literally, with FastChem's H2O VMR (3e-4) as the chemistry provider,
+    and the reference's own run with that chemistry (c1_vmr3e4.npz) at 1e-10."""
+    C = golden("c1_vmr3e4.npz")
+    planet = fa.Planet.from_hot_jupiter()
+    T_ref = 2400.0
+    grid = fa.Grid(planet=planet, T_ref=T_ref)
+    chem = vmr_provider(3e-4)
+    op = grid.load_opacities(opacities=fa.load_example_opacity(grid, scale_factor=1),
+                             chemistry=chem)
+    assert rel(chem(grid.init_temperatures, grid.pressures, ["1H2-16O"],
+                    m_bar=planet.m_bar)["1H2-16O"], C["mmr"]) <= 1e-15
+    k, sigma_scattering = fa.kappa(op, grid.init_temperatures[0], grid.pressures[0], grid.lam,
+                                   m_bar=planet.m_bar, chemistry=chem)
+    assert np.all(k > sigma_scattering)
+    assert sigma_scattering[0] > sigma_scattering[-1]
+    spec, temps, temp_hist, dtaus = grid.emission_spectrum(n_timesteps=1)
+    eng = grid.engine()
+    assert eng.path()["contracted"]            # T-independent provider: the device loop
+    up, down = eng.get_fluxes()
+    # test_core.py:51-56, 58-64, 66-71
+    assert abs(spec.wavelength[spec.flux.argmax()] - 1.1518) <= 0.02
+    assert abs(spec.flux.max() - 1.296e13) <= 0.1e13
+    teff = fa.effective_temperature(grid, spec, dtaus, temps)
+    assert abs(teff - T_ref) <= 200.0
+    # the reference itself under the same chemistry: 1e-10 outright (its one-ulp floor 3e-12)
+    assert_grid_parity(spec.flux, C["spectrum"], up, C["F_up"], down, C["F_down"],
+                       "test_core pins, VMR 3e-4 vs reference", T=temps, ref_T=C["final_T"])
+    assert rel(temp_hist, C["temp_hist"]) <= 1e-10
+    assert rel(dtaus[1:], C["dtaus"][1:]) <= 1e-10
+    assert abs(teff - float(C["Teff"])) <= 1e-6 * float(C["Teff"])
