@@ -105,12 +105,14 @@ def lib():
             raise RuntimeError(f"frei_amd: native library {LIB_PATH} is missing; build it with "
                                "`python -m frei_amd.build` (no CPU fallback exists)")
         if LIB_PATH == _DEFAULT_LIB and os.environ.get("FREI_SKIP_STAMP") != "1":
-            from .build import sources_present, stamp_matches
+            from .build import read_stamp, sources_present, stamp_matches
             # without the csrc sources (an installed package) the stamp cannot be verified: the
             # library is loaded as it is; with them, a library built from other sources is refused
             if sources_present() and not stamp_matches(LIB_PATH):
+                built_by = (read_stamp(LIB_PATH)[1] or "unknown compiler").splitlines()
                 raise RuntimeError(f"frei_amd: {LIB_PATH} was not built from the sources in this "
-                                   "tree (its .stamp hash differs); rebuild with "
+                                   "tree (its .stamp hash differs; it was built by "
+                                   f"{built_by[0] if built_by else '?'}); rebuild with "
                                    "`python -m frei_amd.build`")
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
         for name, (res, args) in SIGNATURES.items():

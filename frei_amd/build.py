@@ -1,9 +1,11 @@
 """Build libfrei_hip.so in-tree for gfx950:  python -m frei_amd.build
 
-The library is rebuilt whenever the SHA-256 of its sources, headers, compiler and flags differs
-from the stamp written beside it (``libfrei_hip.so.stamp``) — not by modification times, which a
-copied tree (the GPU box's snapshot) does not preserve meaningfully.  ``frei_amd._native``
-checks the same stamp at load time and refuses a library built from other sources.
+The library is rebuilt whenever the SHA-256 of its sources, headers and flags — or the compiler
+that built it — differs from the stamp written beside it (``libfrei_hip.so.stamp``: the source
+hash on its first line, the compiler's identity after it), not by modification times, which a
+copied tree (the GPU box's snapshot) does not preserve meaningfully.  ``frei_amd._native`` checks
+the source hash at load time and refuses a library built from other sources; the compiler line is
+only compared at build time (loading runs no compiler) and named in the load error.
 """
 import glob
 import hashlib
@@ -51,10 +53,8 @@ def sources_present():
 
 
 def source_hash(extra_flags=()):
-    """SHA-256 over the sources' names and bytes, the compiler identity and the build command's
-    flags."""
+    """SHA-256 over the sources' names and bytes and the build command's flags."""
     h = hashlib.sha256()
-    h.update(compiler_id().encode() + b"\0")
     for f in source_files():
         h.update(os.path.relpath(f, ROOT).encode() + b"\0")
         with open(f, "rb") as fh:
@@ -64,17 +64,26 @@ def source_hash(extra_flags=()):
     return h.hexdigest()
 
 
-def stamp_matches(lib=LIB):
-    """True when ``lib`` exists and its stamp is the current sources' hash."""
+def read_stamp(lib=LIB):
+    """(source hash, compiler identity) recorded beside ``lib``; (None, None) without a stamp."""
     try:
         with open(lib + ".stamp") as f:
-            return os.path.exists(lib) and f.read().strip() == source_hash()
+            text = f.read()
     except OSError:
-        return False
+        return None, None
+    first, _, rest = text.partition("\n")
+    return first.strip(), rest.strip()
+
+
+def stamp_matches(lib=LIB):
+    """True when ``lib`` exists and its stamp carries the current sources' hash (load-time check:
+    runs no compiler)."""
+    digest, _ = read_stamp(lib)
+    return os.path.exists(lib) and digest == source_hash()
 
 
 def build(verbose=False):
-    if stamp_matches():
+    if stamp_matches() and read_stamp()[1] == compiler_id().strip():
         return LIB
     digest = source_hash()
     # one object per translation unit, compiled in parallel (no relocatable device code: every
@@ -99,7 +108,7 @@ def build(verbose=False):
     for o in objs:
         os.unlink(o)
     with open(STAMP + ".tmp", "w") as f:
-        f.write(digest + "\n")
+        f.write(digest + "\n" + compiler_id().strip() + "\n")
     os.replace(STAMP + ".tmp", STAMP)
     return LIB
 

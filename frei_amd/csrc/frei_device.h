@@ -8,10 +8,6 @@
 
 // The sweeps' coefficient form (frei_kernels.hip StepCoef): 1 = premultiplied by 1/chi and
 // pi_w (two fma per flux update), 0 = the reference's literal association.
-#ifndef FREI_LEAN
-#define FREI_LEAN 1
-#endif
-
 namespace frei {
 
 // CODATA 2018 (astropy 4.3.1, the reference's unit backend), cgs.
@@ -383,20 +379,12 @@ __host__ __device__ inline size_t update_lds_bytes(int nL, int ntn, int S, bool 
   return b;
 }
 
-// Per-block partial sums of a sweep, [blocks][steps x 4] (FREI_PART_BLOCK_MAJOR 1: each block
-// writes its ns x 4 values as whole cache lines; an update workgroup reads its layer's 8 values
-// of every block, one 64-byte span each) or [steps x 4][blocks] (0: the round-1..3 layout).
-#ifndef FREI_PART_BLOCK_MAJOR
-#define FREI_PART_BLOCK_MAJOR 1
-#endif
+// Per-block partial sums of a sweep, [blocks][steps x 4]: each block writes its ns x 4 values
+// as whole cache lines; an update workgroup reads its layer's 8 values of every block, one
+// 64-byte span each (round 4; rounds 1-3 stored [steps x 4][blocks]).
 __host__ __device__ inline int64_t part_at(int idx, int bx, int nbx, int ns4) {
-#if FREI_PART_BLOCK_MAJOR
   (void)nbx;
   return (int64_t)bx * ns4 + idx;
-#else
-  (void)ns4;
-  return (int64_t)idx * nbx + bx;
-#endif
 }
 
 // launchers (frei_kernels.hip)

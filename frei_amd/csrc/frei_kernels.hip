@@ -66,55 +66,17 @@ __device__ unsigned int g_trace_n;
 // record) — instead of one division per update: within 1.5 ulp of the reference's
 // hc / ((lam k) T), which moves spectra and T by < 1e-13.
 //
-// FREI_PLANCK_EXP (default 1): the same value as c1 e / (1 - e) with e = exp(-x), from the
-// transmission's exp (its coefficients are wave-uniform SGPR constants the sweep already holds)
-// instead of an expm1 whose ten coefficients occupied 20 VGPRs per lane: four VALU and 20 VGPRs
-// fewer per update, no range guard (e in [0, 1]: the quotient never overflows, and e underflows
-// to the reference's 0 at x > 745).  Error: a few ulp, growing as ~1 ulp / x for x < 1 (the
+// The value is formed as c1 e / (1 - e) with e = exp(-x), from the transmission's exp (its
+// coefficients are wave-uniform SGPR constants the sweep already holds) instead of an expm1
+// whose ten coefficients occupied 20 VGPRs per lane: four VALU and 20 VGPRs fewer per update,
+// no range guard (e in [0, 1]: the quotient never overflows, and e underflows to the
+// reference's 0 at x > 745).  Error: a few ulp, growing as ~1 ulp / x for x < 1 (the
 // cancellation in 1 - e) — 1e-15 relative at x = 0.1, far inside the 1e-10 parity bar.  A NaN
 // temperature propagates.  Between x = 709.8 (where numpy's expm1 overflows, B = 0) and 745 it
 // returns the subnormal c1 e instead of 0.
-#ifndef FREI_PLANCK_EXP
-#define FREI_PLANCK_EXP 1
-#endif
-__device__ __forceinline__ double planck_e(double c1, double x) {
-  const double e = fm::exp_neg_unclamped(-x);
-  return fm::div(c1 * e, 1.0 - e);
-}
 __device__ __forceinline__ double planck(double c1, double hcl, double iT) {
-#ifdef FREI_MEMONLY
-  return c1 * hcl * iT;
-#elif FREI_PLANCK_EXP
-  return planck_e(c1, hcl * iT);
-#else
-  return fm::div_big(c1, fm::expm1(hcl * iT));
-#endif
-}
-
-#ifndef FREI_EXPM1_VREG
-#define FREI_EXPM1_VREG 1
-#endif
-#ifndef FREI_PI_E1   // E = 1 lanes: pi (1 - w0) / (1 - w0) taken as pi (within an ulp)
-#define FREI_PI_E1 1
-#endif
-// The sweeps' Planck values: expm1 coefficients in VGPRs (fm::Expm1Reg, loaded once), the
-// range-select-free expm1 for exponents <= 600 and an IEEE fallback branch (execz-skipped)
-// for the rare lanes above — cold layers at short wavelengths, where expm1 passes 2^865 and
-// the guard-free division could lose the denormal quotient.
-__device__ __forceinline__ double planck(double c1, double hcl, double iT,
-                                        const fm::Expm1Reg& k) {
-#if FREI_PLANCK_EXP && !defined(FREI_MEMONLY)
-  (void)k;
-  return planck_e(c1, hcl * iT);
-#elif FREI_EXPM1_VREG && !defined(FREI_MEMONLY)
-  const double x = hcl * iT;
-  double B = fm::div(c1, fm::expm1_mid(x < 600.0 ? x : 600.0, k));
-  if (__builtin_expect(!(x <= 600.0), 0)) B = c1 / fm::expm1(x, k);
-  return B;
-#else
-  (void)k;
-  return planck(c1, hcl, iT);
-#endif
+  const double e = fm::exp_neg_unclamped(-(hcl * iT));
+  return fm::div(c1 * e, 1.0 - e);
 }
 
 // twostream.py:97-177 with g_0 = 0 (call sites 389, 518), E() of :70-94.
@@ -398,88 +360,44 @@ __global__ __launch_bounds__(kBlock) void sweep_kernel(SweepArgs a) {
 // Software-pipelined: the next step's 2S table rows and its stale opposite-stream flux
 // are loaded into registers while the current step computes, so HBM latency overlaps the
 // fp64 two-stream arithmetic instead of serialising with it.
-#ifndef FREI_LB_WAVES
-#define FREI_LB_WAVES 1
-#endif
-#ifndef FREI_NT
-#define FREI_NT 0
-#endif
-// Flux-row stores of the sweeps.  FREI_WT_STORE=1 (A/B): system-scope relaxed stores, which
-// gfx950 writes through the L2, so the sweep leaves no dirty flux lines for the end-of-kernel
-// L2 writeback.
-#ifndef FREI_WT_STORE
-#define FREI_WT_STORE 0
-#endif
-__device__ __forceinline__ void flux_store(double* p, double v) {
-#if FREI_WT_STORE == 2   // agent scope: global_store sc1 (write-through to memory, line dropped)
-  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#elif FREI_WT_STORE
-  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#else
-  *p = v;
-#endif
+// (Measured and not adopted, profiles/design_notes_r01_r03.md and profiles/r04/: non-temporal
+// row loads, write-through flux stores.)
+
+// Issue priority by progress: a wave in quarter q of its layer loop runs at priority 3 - q, so
+// waves that started late (second-round blocks) catch up instead of trailing alone at the end
+// of the launch (the hardware otherwise favours the oldest wave).  DESIGN.md §3.
+__device__ __forceinline__ void progress_priority(int k0, int ns) {
+  switch ((4 * k0) / ns) {
+    case 0: __builtin_amdgcn_s_setprio(3); break;
+    case 1: __builtin_amdgcn_s_setprio(2); break;
+    case 2: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+  }
 }
 
-__device__ __forceinline__ double stream_load(const double* p) {
-#if FREI_NT
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
-
-#ifndef FREI_PRIO_PROGRESS
-#define FREI_PRIO_PROGRESS 1
-#endif
-// Scheduling fence of the sweep's load ring (FREI_RING_FENCE=0: none, A/B).
-#ifndef FREI_RING_FENCE
-#define FREI_RING_FENCE 1
-#endif
-__device__ __forceinline__ void ring_fence() {
-#if FREI_RING_FENCE
-  __builtin_amdgcn_sched_barrier(0);
-#endif
-}
+// Scheduling fence of the sweep's load ring.
+__device__ __forceinline__ void ring_fence() { __builtin_amdgcn_sched_barrier(0); }
+__device__ __forceinline__ void store_flux(double* p, double v) { *p = v; }
 // A register-level dependence of a refill's address on the value that consumed the slot (no
 // instruction): sched_barrier only orders the machine scheduler, while instruction selection had
 // already placed the refill loads ahead of the opacity that reads the slot, so the old and new
 // values overlapped and the loop latch copied the four row registers after waiting for their
-// loads (s_waitcnt vmcnt(5..2) + five v_mov_b64 per two steps).  FREI_RING_DEP=0: off (A/B).
-#ifndef FREI_RING_DEP
-#define FREI_RING_DEP 1
-#endif
+// loads (s_waitcnt vmcnt(5..2) + five v_mov_b64 per two steps).
 // (On the element index, not the pointer: a pointer out of an asm is generic, and its loads
 // would become flat loads that also wait on the LDS counter.)
 template <class I>
 __device__ __forceinline__ I after_use(I idx, double used) {
-#if FREI_RING_DEP
   asm volatile("" : "+v"(idx) : "v"(used));
-#else
-  (void)used;
-#endif
   return idx;
 }
 template <class I>
 __device__ __forceinline__ I after_use(I idx, double used, double used2) {
-#if FREI_RING_DEP
   asm volatile("" : "+v"(idx) : "v"(used), "v"(used2));
-#else
-  (void)used;
-  (void)used2;
-#endif
   return idx;
 }
 // A value read on every path (no instruction): a load left pending on a rarely taken path makes
 // the loop's merge blocks wait for everything issued after it (vmcnt is in order).
-__device__ __forceinline__ void consume(double v) {
-#if FREI_RING_DEP
-  asm volatile("" ::"v"(v));
-#else
-  (void)v;
-#endif
-}
+__device__ __forceinline__ void consume(double v) { asm volatile("" ::"v"(v)); }
 
 // Carry-independent part of one step (everything in twostream.py:135-176 except the
 // terms that multiply the carried flux).  Split out so two layers' coefficients form one
@@ -497,61 +415,39 @@ __device__ __forceinline__ int64_t uni(int64_t x) {
   return (int64_t)__double_as_longlong(uni(__longlong_as_double((long long)x)));
 }
 
-// Step parameters that only feed arithmetic (T1, T2, dm, weights, mmr): with
-// FREI_UNI_VGPR they are read from the LDS step table straight into VGPRs (uniform values, a
-// broadcast LDS read) instead of readfirstlane'd into SGPRs: two VALU readfirstlanes fewer
-// per double, and no SGPR pressure from the steps in flight.
-#ifndef FREI_UNI_VGPR
-#define FREI_UNI_VGPR 1
-#endif
-#if FREI_UNI_VGPR
-#define UNIV(x) (x)
-#else
-#define UNIV(x) uni(x)
-#endif
+// (Step parameters that only feed arithmetic — T1, T2, dm, weights, mmr — are read from the
+// LDS step table straight into VGPRs, a broadcast LDS read, not readfirstlane'd into SGPRs.)
 
-// FREI_LEAN (default 1): the step's coefficients premultiplied by 1/chi (and pi_w), so a flux
-// update is two fma on the carried input, F2u = (ic psi) F1u - (ic xi) F2d + (ic pi_w) Xu,
-// instead of ic ((psi F1u - xi F2d) + pi_w Xu): a different association of the same products
-// (an ulp or so, tools/lean_err.py), fewer instructions on the carried chain and four ring
-// values per step in the producer/consumer sweep instead of five.  Every sweep form uses the
-// same coefficients, so they stay bitwise identical to each other.
+// The step's coefficients are premultiplied by 1/chi (and pi_w), so a flux update is two fma on
+// the carried input, F2u = (ic psi) F1u - (ic xi) F2d + (ic pi_w) Xu, instead of
+// ic ((psi F1u - xi F2d) + pi_w Xu): a different association of the same products (an ulp or
+// so, tools/lean_err.py), fewer instructions on the carried chain and four ring values per step
+// in the producer/consumer sweep.  Every sweep form uses the same coefficients, so they stay
+// bitwise identical to each other.
 struct StepCoef {
-  // FREI_LEAN 0: F2u = ic*((psi*F1u - xi*F2d) + Xu), F1d = ic*((psi*F2d - xi*F1u) + Xd)
-  // FREI_LEAN 1: psi, xi, Xu, Xd hold ic*psi, ic*xi, ic*Xu, ic*Xd (ic unused):
-  //              F2u = psi F1u - xi F2d + Xu, F1d = psi F2d - xi F1u + Xd (step_up / step_dn)
-  double psi, xi, ic, Xu, Xd;
+  // psi, xi, Xu, Xd hold ic*psi, ic*xi, ic*Xu, ic*Xd:
+  //   F2u = psi F1u - xi F2d + Xu, F1d = psi F2d - xi F1u + Xd (step_up / step_dn)
+  double psi, xi, Xu, Xd;
   double dtau, Bnext;          // Bnext: Planck value the next layer reuses
   double F_st;                 // stale opposite-stream flux
   int layer, top;
 };
 
 // The flux update of one step from its coefficients (twostream.py:161-176).
-__device__ __forceinline__ double step_up(double psi, double xi, double ic, double Xu,
-                                          double F1u, double F2d) {
-#if FREI_LEAN
-  (void)ic;
+__device__ __forceinline__ double step_up(double psi, double xi, double Xu, double F1u,
+                                          double F2d) {
   return __builtin_fma(psi, F1u, __builtin_fma(-xi, F2d, Xu));
-#else
-  return ic * ((psi * F1u - xi * F2d) + Xu);
-#endif
 }
-__device__ __forceinline__ double step_dn(double psi, double xi, double ic, double Xd,
-                                          double F1u, double F2d) {
-#if FREI_LEAN
-  (void)ic;
+__device__ __forceinline__ double step_dn(double psi, double xi, double Xd, double F1u,
+                                          double F2d) {
   return __builtin_fma(psi, F2d, __builtin_fma(-xi, F1u, Xd));
-#else
-  return ic * ((psi * F2d - xi * F1u) + Xd);
-#endif
 }
 
 // Terms after E (twostream.py:143-176), same expression order as two_stream().  pi_w =
-// pi (1 - w0) / (E - w0) comes from the caller; 1 / chi is formed within an ulp (it scales
-// the whole update, nothing cancels after it); the transmission's exp argument is <= 0.
-// NF: the step's inputs cannot be NaN (contracted-table sweeps), so exp's clamp is a max.
-// FREI_LEAN: B1, B2 and q carry the factor pi (c1 = pi 2hc^2/lam^5) and pi_w is the remaining
-// (1 - w0) / (E - w0) (exactly 1 where E = 1); the coefficients come out premultiplied by 1/chi.
+// pi (1 - w0) / (E - w0) comes from the caller (pi itself where E = 1); 1 / chi is formed
+// within an ulp (it scales the whole update, nothing cancels after it); the transmission's exp
+// argument is <= 0.  NF: the step's inputs cannot be NaN (contracted-table sweeps), so exp's
+// clamp is a max.  The coefficients come out premultiplied by 1/chi (and pi_w): StepCoef.
 template <bool NF = false>
 __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, double B2,
                                           double sq, double r, double q, double pi_w,
@@ -565,7 +461,6 @@ __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, dou
   const double Tr2 = Tr * Tr;
   const double zm2 = zm * zm;
   const double zp2 = zp * zp;
-#if FREI_LEAN
   // chi, xi, psi and the source brackets exactly as the reference forms them: their rounding
   // errors are correlated ((chi - psi) - xi cancels to O(dtau^2) in thin layers), so rewriting
   // any of them by an algebraic identity (psi = -r Tr, an fma for chi, (xi + psi) - chi as
@@ -578,19 +473,8 @@ __device__ __forceinline__ void coef_tail(double w0, double dtau, double B1, dou
   const double icw = ic * pi_w;
   c.psi = ic * psi;
   c.xi = ic * xi;
-  c.ic = 1.0;
   c.Xu = icw * ((B2 * u - psi * B1) + q * ((chi - psi) - xi));
   c.Xd = icw * ((B1 * u - psi * B2) + q * ((xi + psi) - chi));
-#else
-  const double chi = zm2 * Tr2 - zp2;
-  const double xi = (zp * zm) * (1.0 - Tr2);
-  const double psi = (zm2 - zp2) * Tr;
-  c.psi = psi;
-  c.xi = xi;
-  c.ic = fm::rcp_nr(chi);
-  c.Xu = pi_w * ((B2 * (chi + xi) - psi * B1) + q * ((chi - psi) - xi));
-  c.Xd = pi_w * ((B1 * (chi + xi) - psi * B2) + q * ((xi + psi) - chi));
-#endif
   c.dtau = dtau;
 }
 
@@ -612,11 +496,7 @@ __device__ __forceinline__ CoefHead coef_head_e1(double w0, double dtau, double 
   h.sq = fm::sqrt_pos(Emw);
   h.r = h.sq;
   h.q = fm::div(B1 - B2, dtau) * 0.5;   // = div(div(B1 - B2, dtau), 2 E) at E = 1
-#if FREI_PI_E1 || FREI_LEAN
-  h.pi_w = kPi;
-#else
-  h.pi_w = fm::div(kPi * (1.0 - w0), Emw);
-#endif
+  h.pi_w = kPi;   // pi (1 - w0) / (1 - w0): pi within an ulp
   return h;
 }
 __device__ __forceinline__ void coef_head_general(double w0, double dtau, double B1, double B2,
@@ -762,9 +642,6 @@ __device__ __forceinline__ void sweep_fast_body(
   // staged partial sums (red_rows 2) reduce a pair of steps: the pair is one coefficient block
   // (PD = 2), or the two one-step blocks of a trip (PD = 1, PF = 2: fewer registers per wave)
   constexpr bool kPairs = PD == 2 || (PD == 1 && PF == 2);
-#if defined(FREI_ISA_E1ONLY) || defined(FREI_ISA_STAGED)   // ISA-histogram build: the staged partial sums, as the 500k sweep runs
-  a.red_rows = 2;
-#endif
   // no NaN reaches the coefficients: the contracted table is built from NaN-free tables, and
   // with S > 1 the tables were scanned (NaN-free, or NANCHK's nansum zeroes NaN terms); only a
   // single per-species table keeps the reference's NaN propagation (Q8)
@@ -797,7 +674,6 @@ __device__ __forceinline__ void sweep_fast_body(
   const double c1 = a.c1[j], hcl = a.hcl[j], sig = a.sig[j];
   const double wt = act ? a.wtr[j] : 0.0;
   const int ns = a.n_steps;
-  const fm::Expm1Reg ek = fm::expm1_regs();
   // Shared brackets: stage the whole step table (ns x 120 B) in LDS once, so every step
   // reads its uniform parameters at LDS latency instead of scalar loads that miss the
   // K$ and L2 of a freshly scheduled CU (the step table was written by the update kernel).
@@ -826,40 +702,25 @@ __device__ __forceinline__ void sweep_fast_body(
   // vmcnt bookkeeping stays static.
   auto load_rows = [&](int k, double (&v)[2 * S], double dep = 0.0) {
     k = k < ns ? k : ns - 1;
-#ifdef FREI_CACHEONLY   // diagnostic build: same instructions, loads from a cache-resident 32 KB
-    {
-      const int64_t jj = j & 2047;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        v[2 * s] = stream_load(a.tab[s] + jj + (k & 1) * 2048);
-        v[2 * s + 1] = stream_load(a.tab[s] + jj + 4096);
-      }
-      return;
-    }
-#endif
     if constexpr (SH) {
       const int64_t off = uni(sp[k].off);
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const double* r = a.tab[s] + after_use(off + j, dep);
-        v[2 * s] = stream_load(r);
-        v[2 * s + 1] = stream_load(r + a.pitch);
+        v[2 * s] = *(r);
+        v[2 * s + 1] = *(r + a.pitch);
       }
       return;
     }
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const double* r = a.tab[s] + after_use(st[k].off[s] + j, dep);
-      v[2 * s] = stream_load(r);
-      v[2 * s + 1] = stream_load(r + a.pitch);
+      v[2 * s] = *(r);
+      v[2 * s + 1] = *(r + a.pitch);
     }
   };
   auto load_stale = [&](int k, double& stale) {
     k = k < ns ? k : ns - 1;
-#ifdef FREI_CACHEONLY
-    stale = Fu[(j & 2047) + (k & 1) * 2048];
-    return;
-#endif
     const int i = layer_of(k);
     const double* src = (DIR == kEmit) ? (top_of(k) ? a.ftoa : Fd + (int64_t)(i + 1) * nl)
                                        : Fu + (int64_t)i * nl;
@@ -876,8 +737,8 @@ __device__ __forceinline__ void sweep_fast_body(
       if constexpr (SH) {
         // (0 + a) + b == a + b for the non-negative table terms; the contracted table (MM1)
         // carries mmr = 1, whose product is the identity
-        const double acc = vlo * UNIV(sp[kk].wlo) + vhi * UNIV(sp[kk].whi);
-        ops = MM1 ? acc : UNIV(sp[kk].mmr[s]) * acc;
+        const double acc = vlo * (sp[kk].wlo) + vhi * (sp[kk].whi);
+        ops = MM1 ? acc : (sp[kk].mmr[s]) * acc;
       } else {
         const double acc = vlo * st[kk].wlo[s] + vhi * st[kk].whi[s];
         ops = MM1 ? acc : st[kk].mmr[s] * acc;
@@ -895,15 +756,15 @@ __device__ __forceinline__ void sweep_fast_body(
   // loop consumes (and refills) its row slots after both steps' Planck chains.
   auto planck_new = [&](int k) {
     const int kk = k < ns ? k : ns - 1;
-    if constexpr (SH) return planck(c1, hcl, DIR == kEmit ? UNIV(sp[kk].iT2) : UNIV(sp[kk].iT1), ek);
-    else return planck(c1, hcl, DIR == kEmit ? st[kk].iT2 : st[kk].iT1, ek);
+    if constexpr (SH) return planck(c1, hcl, DIR == kEmit ? (sp[kk].iT2) : (sp[kk].iT1));
+    else return planck(c1, hcl, DIR == kEmit ? st[kk].iT2 : st[kk].iT1);
   };
   auto coef = [&](int k, double tot, double Bprev, double X, StepCoef& c, PreCoef& pc) {
     const int kk = k < ns ? k : ns - 1;
     double dm;
     c.layer = layer_of(kk);
     c.top = top_of(kk);
-    if constexpr (SH) dm = UNIV(sp[kk].dm);
+    if constexpr (SH) dm = (sp[kk].dm);
     else dm = st[kk].dm;
     const double kap = tot + sig;
     const double dtau = dm * kap;
@@ -927,13 +788,6 @@ __device__ __forceinline__ void sweep_fast_body(
   // w0 <= 0.1 (a wave-uniform branch, so the group stays one straight-line block), else the
   // general form (bit-identical on the E = 1 lanes).
   auto coefB = [&](PreCoef (&pc)[PD], StepCoef (&c)[PD]) {
-#ifdef FREI_MEMONLY  // diagnostic build: same memory traffic, trivial arithmetic
-#pragma unroll
-    for (int b = 0; b < PD; ++b) {
-      c[b].psi = 0.5; c[b].xi = pc[b].w0; c[b].ic = 1.0; c[b].Xu = pc[b].B2 + pc[b].dtau;
-      c[b].Xd = pc[b].B1; c[b].dtau = pc[b].dtau;
-    }
-#else
     bool e1 = true;
     CoefHead h[PD];
 #pragma unroll
@@ -941,9 +795,6 @@ __device__ __forceinline__ void sweep_fast_body(
       e1 = e1 && !(pc[b].w0 > 0.1);
       h[b] = coef_head_e1(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2);
     }
-#ifdef FREI_ISA_E1ONLY   // ISA-histogram build (tools/isa_hist.py): the E = 1 path alone
-    e1 = true;
-#endif
     if (!__all(e1)) {   // rare: one step at a time (registers, not ILP)
 #pragma unroll
       for (int b = 0; b < PD; ++b) {
@@ -956,7 +807,6 @@ __device__ __forceinline__ void sweep_fast_body(
     for (int b = 0; b < PD; ++b)
       coef_tail<kNaNFree>(pc[b].w0, pc[b].dtau, pc[b].B1, pc[b].B2, h[b].sq, h[b].r, h[b].q,
                           h[b].pi_w, c[b]);
-#endif
   };
 
   // Carry-dependent finish of step k: fluxes, stores, bolometric partials.
@@ -967,8 +817,8 @@ __device__ __forceinline__ void sweep_fast_body(
     consume(F_st);
     double F1u, F2d;
     if (DIR == kEmit) { F1u = carry; F2d = F_st; } else { F2d = carry; F1u = F_st; }
-    const double F2u = step_up(c.psi, c.xi, c.ic, c.Xu, F1u, F2d);
-    const double F1d = step_dn(c.psi, c.xi, c.ic, c.Xd, F1u, F2d);
+    const double F2u = step_up(c.psi, c.xi, c.Xu, F1u, F2d);
+    const double F1d = step_dn(c.psi, c.xi, c.Xd, F1u, F2d);
     if (k >= ns) return;
     const int i = c.layer;
     if (act) {
@@ -976,8 +826,8 @@ __device__ __forceinline__ void sweep_fast_body(
       // are rewritten by absorb before any read, absorb's F_up rows >= 2 by the next emit).
       const bool st_up = (DIR == kEmit) ? !c.top : (!a.live_only || i == 0);
       const bool st_dn = (DIR == kAbsorb) || !a.live_only || c.top;
-      if (st_up) flux_store(Fu + (int64_t)(i + 1) * nl + j, F2u);
-      if (st_dn) flux_store(Fd + (int64_t)i * nl + j, F1d);
+      if (st_up) store_flux(Fu + (int64_t)(i + 1) * nl + j, F2u);
+      if (st_dn) store_flux(Fd + (int64_t)i * nl + j, F1d);
       if (dtaus) dtaus[(int64_t)(k + 1) * nl + j] = c.dtau;
     }
     if (kPairs && a.red_rows == 2) {   // staged: reduced per pair of steps (stage_reduce)
@@ -1009,10 +859,10 @@ __device__ __forceinline__ void sweep_fast_body(
     const double iT10 = SH ? sp[0].iT1 : st[0].iT1, iT20 = SH ? sp[0].iT2 : st[0].iT2;
     if (DIR == kEmit) {
       carry = Fu[(int64_t)l0 * nl + j];
-      Bc = planck(c1, hcl, iT10, ek);
+      Bc = planck(c1, hcl, iT10);
     } else {
       carry = Fd[(int64_t)(l0 + 1) * nl + j];
-      Bc = planck(c1, hcl, iT20, ek);
+      Bc = planck(c1, hcl, iT20);
     }
   }
   // PD steps in flight: their loads are issued PD steps ahead, their coefficients form one
@@ -1034,22 +884,7 @@ __device__ __forceinline__ void sweep_fast_body(
   for (int b = 0; b < PF; ++b) load_stale(b, sb[b]);
   ring_fence();
   for (int k0 = 0; k0 < ns; k0 += PF) {
-#if FREI_PRIO_PROGRESS
-    // issue priority by progress (FREI_PRIO_PROGRESS 1): a wave early in its layer loop outranks
-    // one near its end, so waves that started late (second-round blocks) catch up instead of
-    // trailing alone at the end of the launch (the hardware otherwise favours the oldest wave);
-    // 2: a rotating priority (trip + block index) — no wave wins every arbitration; 3: steps
-    // at 1/2, 3/4, 7/8 of the loop; 4: rotating with the block's dispatch round (A/B)
-    switch (FREI_PRIO_PROGRESS == 2   ? ((k0 >> 1) + bx) & 3
-            : FREI_PRIO_PROGRESS == 4 ? ((k0 >> 1) + (bx >> 8)) & 3
-            : FREI_PRIO_PROGRESS == 3 ? (2 * k0 < ns ? 0 : 4 * k0 < 3 * ns ? 1 : 8 * k0 < 7 * ns ? 2 : 3)
-                                      : (4 * k0) / ns) {
-      case 0: __builtin_amdgcn_s_setprio(3); break;
-      case 1: __builtin_amdgcn_s_setprio(2); break;
-      case 2: __builtin_amdgcn_s_setprio(1); break;
-      default: __builtin_amdgcn_s_setprio(0); break;
-    }
-#endif
+    progress_priority(k0, ns);
 #pragma unroll
   for (int g = 0; g < PF / PD; ++g) {
     const int k = k0 + g * PD;
@@ -1114,7 +949,7 @@ __device__ __forceinline__ void sweep_fast_body(
 }
 
 template <int DIR, int S, int PD, bool NANCHK, bool SH, bool MM1, int PF>
-__global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_kernel(
+__global__ __launch_bounds__(kBlock, 1) void sweep_fast_kernel(
     FastArgs a, const FastStep* __restrict__ st, const FastStepS* __restrict__ ss,
     double* __restrict__ Fu, double* __restrict__ Fd, double* __restrict__ part,
     double* __restrict__ dtaus) {
@@ -1187,7 +1022,6 @@ __device__ __forceinline__ void sweep_group_body(
   const double c1 = a.c1[j], hcl = a.hcl[j], sig = a.sig[j];
   const double wt = act ? a.wtr[j] : 0.0;
   const int ns = a.n_steps;
-  const fm::Expm1Reg ek = fm::expm1_regs();
   const double* __restrict__ tab = a.tab[0];
   double* lss = red + red_lds_doubles(a.red_rows, ns, NW);
   {
@@ -1234,8 +1068,8 @@ __device__ __forceinline__ void sweep_group_body(
     P.wh = st.whi;
     P.dm = st.dm;
     P.iT = DIR == kEmit ? st.iT2 : st.iT1;
-    P.vlo = stream_load(r);
-    P.vhi = stream_load(r + a.pitch);
+    P.vlo = *(r);
+    P.vhi = *(r + a.pitch);
     kr += Q;
   };
   auto load_stale = [&](Pre& P) {
@@ -1251,10 +1085,10 @@ __device__ __forceinline__ void sweep_group_body(
     const int l0 = sp[0].layer;
     if (DIR == kEmit) {
       carry = Fu[(int64_t)l0 * nl + j];
-      carryB = planck(c1, hcl, sp[0].iT1, ek);
+      carryB = planck(c1, hcl, sp[0].iT1);
     } else {
       carry = Fd[(int64_t)(l0 + 1) * nl + j];
-      carryB = planck(c1, hcl, sp[0].iT2, ek);
+      carryB = planck(c1, hcl, sp[0].iT2);
     }
   }
   struct GroupA {
@@ -1269,7 +1103,7 @@ __device__ __forceinline__ void sweep_group_body(
     // each lane forms its step's new Planck value; the group gathers them and resolves
     // (B1, B2) of its steps in order (emit: B2 is new and becomes the next B1; absorb: B1 is
     // new and becomes the next B2; emit's top step keeps B2 = B1)
-    const double X = planck(c1, hcl, P.iT, ek);
+    const double X = planck(c1, hcl, P.iT);
     // contracted table: mmr = 1, and (0 + a) + b == a + b for its non-negative terms
     const double kap = (P.vlo * P.wl + P.vhi * P.wh) + sig;
     A.dtau = P.dm * kap;
@@ -1303,11 +1137,11 @@ __device__ __forceinline__ void sweep_group_body(
     // the two fluxes of a step from its carried input (same expressions as the one-lane form)
     auto flux_up = [&](double in) {   // F_2_up
       const double F1u = (DIR == kEmit) ? in : F_st, F2d = (DIR == kEmit) ? F_st : in;
-      return step_up(c.psi, c.xi, c.ic, c.Xu, F1u, F2d);
+      return step_up(c.psi, c.xi, c.Xu, F1u, F2d);
     };
     auto flux_dn = [&](double in) {   // F_1_down
       const double F1u = (DIR == kEmit) ? in : F_st, F2d = (DIR == kEmit) ? F_st : in;
-      return step_dn(c.psi, c.xi, c.ic, c.Xd, F1u, F2d);
+      return step_dn(c.psi, c.xi, c.Xd, F1u, F2d);
     };
     // the carried chain runs through the group's steps in order, each step in its own lane
     // (q == r); only the carried flux is formed in the chain, the other one once afterwards
@@ -1337,8 +1171,8 @@ __device__ __forceinline__ void sweep_group_body(
       const bool last = k == ns - 1;
       const bool st_up = (DIR == kEmit) ? !last : (!a.live_only || last);
       const bool st_dn = (DIR == kAbsorb) || !a.live_only || last;
-      if (st_up) flux_store(pu, F2u);
-      if (st_dn) flux_store(pd, F1d);
+      if (st_up) store_flux(pu, F2u);
+      if (st_dn) store_flux(pd, F1d);
       if (dtaus) *pt = c.dtau;
     }
     pu += rstep;
@@ -1519,17 +1353,7 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
   ring_fence();
   double* tile = red + (int64_t)(kBlock / 64) * ns * 4;
   for (int k0 = 0; k0 < ns; k0 += 2) {
-#if FREI_PRIO_PROGRESS
-    switch (FREI_PRIO_PROGRESS == 2   ? ((k0 >> 1) + bx) & 3
-            : FREI_PRIO_PROGRESS == 4 ? ((k0 >> 1) + (bx >> 8)) & 3
-            : FREI_PRIO_PROGRESS == 3 ? (2 * k0 < ns ? 0 : 4 * k0 < 3 * ns ? 1 : 8 * k0 < 7 * ns ? 2 : 3)
-                                      : (4 * k0) / ns) {
-      case 0: __builtin_amdgcn_s_setprio(3); break;
-      case 1: __builtin_amdgcn_s_setprio(2); break;
-      case 2: __builtin_amdgcn_s_setprio(1); break;
-      default: __builtin_amdgcn_s_setprio(0); break;
-    }
-#endif
+    progress_priority(k0, ns);
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       const int k = k0 + g;
@@ -1566,10 +1390,7 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
       }
       CoefHead ha = coef_head_e1(pa.w0, pa.dtau, pa.B1, pa.B2);
       CoefHead hb = coef_head_e1(pb.w0, pb.dtau, pb.B1, pb.B2);
-      bool e1 = !(pa.w0 > 0.1) && !(pb.w0 > 0.1);
-#ifdef FREI_ISA_E1ONLY
-      e1 = true;
-#endif
+      const bool e1 = !(pa.w0 > 0.1) && !(pb.w0 > 0.1);
       if (!__all(e1)) {   // rare: one wavelength at a time (registers, not ILP)
         ring_fence();
         coef_head_general(pa.w0, pa.dtau, pa.B1, pa.B2, ha);
@@ -1585,10 +1406,10 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
       consume(Fst.x);
       consume(Fst.y);
       const d2 F1u = (DIR == kEmit) ? carry : Fst, F2d = (DIR == kEmit) ? Fst : carry;
-      const d2 F2u = {step_up(ca.psi, ca.xi, ca.ic, ca.Xu, F1u.x, F2d.x),
-                      step_up(cb.psi, cb.xi, cb.ic, cb.Xu, F1u.y, F2d.y)};
-      const d2 F1d = {step_dn(ca.psi, ca.xi, ca.ic, ca.Xd, F1u.x, F2d.x),
-                      step_dn(cb.psi, cb.xi, cb.ic, cb.Xd, F1u.y, F2d.y)};
+      const d2 F2u = {step_up(ca.psi, ca.xi, ca.Xu, F1u.x, F2d.x),
+                      step_up(cb.psi, cb.xi, cb.Xu, F1u.y, F2d.y)};
+      const d2 F1d = {step_dn(ca.psi, ca.xi, ca.Xd, F1u.x, F2d.x),
+                      step_dn(cb.psi, cb.xi, cb.Xd, F1u.y, F2d.y)};
       if (k < ns) {
         const int i = layer_of(k);
         if (act) {
@@ -1717,7 +1538,7 @@ void launch_sweep_group(int dir, int Q, int NW, const FastArgs& a, int nblocks,
 // for bit.  One contracted table (K3, mmr = 1); the step records come from the global step table
 // through scalar loads.
 constexpr int kPipeP = 3;    // producer waves per consumer wave
-constexpr int kPipeNV = FREI_LEAN ? 4 : 5;   // psi, xi, Xu, Xd (+ ic: FREI_LEAN 0)
+constexpr int kPipeNV = 4;   // psi, xi, Xu, Xd
 constexpr int kStepDoubles = (int)(sizeof(FastStepS) / sizeof(double));
 __host__ __device__ inline int64_t pipe_lds_doubles(int NC, int M, int ns) {
   return (int64_t)NC * 2 * (kPipeP * M) * kPipeNV * 64 + (int64_t)NC * 2 * 4 * kStageRow +
@@ -1755,26 +1576,12 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
   const int sub = wv >> 2;    // 64-wavelength chunk of the block
   // 0 .. 2: producer, 3: consumer.  Waves w and w + 4 share a SIMD (profiles/r03/simd_map.txt),
   // so role = w & 3 would put all four consumers on one SIMD and the producers' work on the
-  // other three.  The roles rotate per chunk (FREI_PIPE_ROT: every SIMD holds three producers
-  // and one consumer) and the consumer issues first (FREI_PIPE_PRIO: its chain paces the
-  // phase): together −4 µs per sweep at 62.5k λ (loop 33.2 → 29.6 µs,
-  // profiles/r03/pipe_layout/); either alone is no faster.
-#ifndef FREI_PIPE_ROT
-#define FREI_PIPE_ROT 1
-#endif
-#ifndef FREI_PIPE_RING_AHEAD
-#define FREI_PIPE_RING_AHEAD 1
-#endif
-#ifndef FREI_PIPE_SPF   // phases ahead the consumer loads its stale fluxes (1 or 2)
-#define FREI_PIPE_SPF 1
-#endif
-#ifndef FREI_PIPE_PRIO
-#define FREI_PIPE_PRIO 2
-#endif
-  const int role = FREI_PIPE_ROT ? ((wv + sub) & 3) : (wv & 3);
-#if FREI_PIPE_PRIO
-  if (role == kPipeP) __builtin_amdgcn_s_setprio(FREI_PIPE_PRIO);
-#endif
+  // other three.  The roles rotate per chunk (every SIMD holds three producers and one
+  // consumer) and the consumer issues first (priority 2: its chain paces the phase): together
+  // −4 µs per sweep at 62.5k λ (loop 33.2 → 29.6 µs, profiles/r03/pipe_layout/); either alone
+  // is no faster.
+  const int role = (wv + sub) & 3;
+  if (role == kPipeP) __builtin_amdgcn_s_setprio(2);
   const int64_t nl = a.n_lam;
   const int64_t j0 = (int64_t)bx * (64 * NC) + sub * 64 + lane;
   const bool act = j0 < nl;
@@ -1804,7 +1611,6 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
     // ---------------- producer
     const int p = role;
     const double c1 = a.c1[j], hcl = a.hcl[j], sig = a.sig[j];
-    const fm::Expm1Reg ek = fm::expm1_regs();
     const double* __restrict__ tabj = a.tab[0] + j;
     // a phase's table rows and step parameters, loaded PF phases ahead (two buffers when
     // PF = 2: phases alternate between them, the loop below is unrolled by two)
@@ -1819,8 +1625,8 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
         const int k = min(ph * G + p * M + i, ns - 1);
         const FastStepS& st = lrec[k];
         const double* r = tabj + st.off;
-        b.vlo[i] = stream_load(r);
-        b.vhi[i] = stream_load(r + a.pitch);
+        b.vlo[i] = *(r);
+        b.vhi[i] = *(r + a.pitch);
         b.wl[i] = st.wlo;
         b.wh[i] = st.whi;
         b.dm[i] = st.dm;
@@ -1834,7 +1640,7 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
       StepCoef c[M];
       // the Planck value the first step reuses in the one-lane form: emit B(T1), absorb
       // B(T2) of step kb (the same inverse temperature as the previous step's new one)
-      double Bp = planck(c1, hcl, b.iT0, ek);
+      double Bp = planck(c1, hcl, b.iT0);
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const double kap = (b.vlo[i] * b.wl[i] + b.vhi[i] * b.wh[i]) + sig;
@@ -1844,11 +1650,11 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
         if (DIR == kEmit) {
           const bool top = kb + i >= ns - 1;
           pc[i].B1 = Bp;
-          pc[i].B2 = top ? Bp : planck(c1, hcl, b.iTn[i], ek);
+          pc[i].B2 = top ? Bp : planck(c1, hcl, b.iTn[i]);
           Bp = pc[i].B2;
         } else {
           pc[i].B2 = Bp;
-          pc[i].B1 = planck(c1, hcl, b.iTn[i], ek);
+          pc[i].B1 = planck(c1, hcl, b.iTn[i]);
           Bp = pc[i].B1;
         }
       }
@@ -1857,15 +1663,6 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
       bool e1 = true;
 #pragma unroll
       for (int i = 0; i < M; ++i) e1 = e1 && !(pc[i].w0 > 0.1);
-#ifdef FREI_PIPE_NOPROD   // diagnostic ablation build: trivial coefficients, same loads / stores
-      if (true) {
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-          c[i].psi = pc[i].w0; c[i].xi = pc[i].dtau; c[i].ic = 0.5; c[i].Xu = pc[i].B1;
-          c[i].Xd = pc[i].B2; c[i].dtau = pc[i].dtau;
-        }
-      } else
-#endif
       {
         CoefHead h[M];
 #pragma unroll
@@ -1887,7 +1684,6 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
         *rslot(ph, s, 1) = c[i].xi;
         *rslot(ph, s, 2) = c[i].Xu;
         *rslot(ph, s, 3) = c[i].Xd;
-        if constexpr (kPipeNV == 5) *rslot(ph, s, kPipeNV - 1) = c[i].ic;
         if (dtaus && act && kb + i < ns) dtaus[(int64_t)(kb + i + 1) * nl + j] = c[i].dtau;
       }
     };
@@ -1921,34 +1717,28 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
       const double* src = (DIR == kEmit)
                               ? (k == ns - 1 ? a.ftoa : Fd + (int64_t)(layer + 1) * nl)
                               : Fu + (int64_t)layer * nl;
-#ifdef FREI_PIPE_STALE_HOT   // diagnostic ablation build: stale loads from one cached row
-      return a.ftoa[j] + 0.0 * src[0];
-#else
       return src[j];
-#endif
     };
     double* t0 = tile + (int64_t)sub * 2 * 4 * kStageRow;
     // step i of phase q: the carried chain, flux stores and staged bolometric terms (a pair's
     // 8 sums after its second step)
-    // (rv: the step's psi, xi, Xu, Xd (, ic), read from the ring with the rest of its phase's)
+    // (rv: the step's psi, xi, Xu, Xd, read from the ring with the rest of its phase's)
     auto step = [&](int q, int i, double stv, const double (&rv)[kPipeNV]) {
       const int k = q * G + i;
       if (k < ns) {
-        const double psi = rv[0], xi = rv[1], Xu = rv[2], Xd = rv[3], ic = rv[kPipeNV - 1];
+        const double psi = rv[0], xi = rv[1], Xu = rv[2], Xd = rv[3];
         double F1u, F2d;
         if (DIR == kEmit) { F1u = carry; F2d = stv; } else { F2d = carry; F1u = stv; }
-        const double F2u = step_up(psi, xi, ic, Xu, F1u, F2d);
-        const double F1d = step_dn(psi, xi, ic, Xd, F1u, F2d);
+        const double F2u = step_up(psi, xi, Xu, F1u, F2d);
+        const double F1d = step_dn(psi, xi, Xd, F1u, F2d);
         const int layer = step_layer(DIR, k, nL);
         const bool top = DIR == kEmit && k == ns - 1;
-#ifndef FREI_PIPE_NOSTORE   // diagnostic ablation build: no flux stores
         if (act) {
           const bool st_up = (DIR == kEmit) ? !top : (!a.live_only || layer == 0);
           const bool st_dn = (DIR == kAbsorb) || !a.live_only || top;
-          if (st_up) flux_store(Fu + (int64_t)(layer + 1) * nl + j, F2u);
-          if (st_dn) flux_store(Fd + (int64_t)layer * nl + j, F1d);
+          if (st_up) store_flux(Fu + (int64_t)(layer + 1) * nl + j, F2u);
+          if (st_dn) store_flux(Fd + (int64_t)layer * nl + j, F1d);
         }
-#endif
         double* t = t0 + ((k & 1) * 4) * kStageRow + lane;
         t[0] = wt * F2u;
         t[kStageRow] = wt * F2d;
@@ -1956,11 +1746,7 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
         t[3 * kStageRow] = wt * F1d;
         carry = (DIR == kEmit) ? F2u : F1d;
       }
-#ifdef FREI_PIPE_NORED   // diagnostic ablation build: no bolometric reduction
-      if (false) {
-#else
       if (i & 1) {   // the pair's 8 (step, quantity) sums: the one-lane staged reduction
-#endif
         __builtin_amdgcn_wave_barrier();
         const int o = lane >> 3;
         const double* t = t0 + ((o >> 2) * 4 + (o & 3)) * kStageRow + (lane & 7);
@@ -1976,51 +1762,19 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
       }
     };
     // the phase's ring values, all read before its first step: one LDS round trip per phase
-    // instead of one per step on the carried chain (FREI_PIPE_RING_AHEAD 0: per step)
+    // instead of one per step on the carried chain
     auto read_ring = [&](int q, double (&rv)[G][kPipeNV]) {
 #pragma unroll
       for (int i = 0; i < G; ++i)
 #pragma unroll
         for (int v = 0; v < kPipeNV; ++v) rv[i][v] = *rslot(q, i, v);
-#if FREI_PIPE_RING_AHEAD
       __builtin_amdgcn_sched_barrier(0);   // keep the reads together, ahead of the chain
-#endif
     };
-#if FREI_PIPE_SPF == 2
-    // stale fluxes loaded two phases ahead: two register buffers (phases alternate, the loop
-    // is unrolled by two), each element refilled right after its step has used it
-    double sA[G], sB[G];
-#pragma unroll
-    for (int i = 0; i < G; ++i) sA[i] = stale(0, i);
-#pragma unroll
-    for (int i = 0; i < G; ++i) sB[i] = stale(1, i);
-    auto consume = [&](int q, double (&sv)[G]) {
-      double rv[G][kPipeNV];
-      read_ring(q, rv);
-#pragma unroll
-      for (int i = 0; i < G; ++i) {
-        step(q, i, sv[i], rv[i]);
-        sv[i] = stale(q + 2, i);
-      }
-    };
-    for (int ph = 0; ph <= nph; ph += 2) {   // nph + 1 barriers, like the producers'
-      if (ph >= 1) consume(ph - 1, sB);
-      __syncthreads();
-      if (ph + 1 <= nph) {
-        consume(ph, sA);
-        __syncthreads();
-      }
-    }
-#else
     double stn[G];   // stale opposite-stream fluxes of the next phase
 #pragma unroll
     for (int i = 0; i < G; ++i) stn[i] = stale(0, i);
     for (int ph = 0; ph <= nph; ++ph) {
-#ifdef FREI_PIPE_NOCONS   // diagnostic ablation build: the consumer only meets the barriers
-      if (false) {
-#else
       if (ph >= 1) {
-#endif
         const int q = ph - 1;   // phase consumed now
         double stc[G];
 #pragma unroll
@@ -2034,7 +1788,6 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
       }
       __syncthreads();
     }
-#endif
   }
   TRACE_MARK(2);
   __syncthreads();
@@ -2098,9 +1851,6 @@ size_t pipe_lds_bytes(int NC, int M, int ns) {
 }
 
 // ---------------------------------------------------------------- P2P exchange
-#ifndef FREI_P2P_FENCE
-#define FREI_P2P_FENCE 1
-#endif
 // System-scope stores of a value and then its flag into every rank's mailbox (P2PPush): the
 // release fence orders the value stores before the flag stores for any observer; the
 // explicit wait keeps the compiler from dropping the fence's completion wait (gfx950 hazard,
@@ -2114,12 +1864,10 @@ __device__ __forceinline__ void p2p_push_values(const P2PPush& p, int64_t idx, c
       __hip_atomic_store(dst + idx + k, __builtin_bit_cast(uint64_t, v[k]), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
-#if FREI_P2P_FENCE
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-#endif
   // The system-scope release orders the value stores before the flag stores for any observer.
   // (The payload is only the write-through system-scope stores above, so the completion wait
-  // alone would order them too; FREI_P2P_FENCE=0 drops the fence: measured no different,
+  // alone would order them too; without the fence: measured no different,
   // profiles/r02_p2p_after_fix.txt, so the canonical release stays.)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (int r = 0; r < p.nranks; ++r) {
@@ -2149,14 +1897,7 @@ __device__ __forceinline__ void p2p_wait(const P2PWait& w, int r, int64_t idx, l
 // The acquire that pairs with p2p_push_values' system-scope release: issued after the flag
 // waits and before any p2p_value, so the value loads cannot be performed (by the compiler or
 // the memory system) ahead of the flag loads that observed this sweep's sequence number.
-#ifndef FREI_P2P_ACQ   // A/B only (0: no fence; the value loads then rely on issue order)
-#define FREI_P2P_ACQ 1
-#endif
-__device__ __forceinline__ void p2p_acquire() {
-#if FREI_P2P_ACQ
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-#endif
-}
+__device__ __forceinline__ void p2p_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
 
 // Rank r's value idx of this sweep (after p2p_wait + p2p_acquire); the mailbox is uncached
 // and the load is system-scope, so it reads memory.
@@ -2186,10 +1927,7 @@ void launch_p2p_handshake(const P2PPush& push, const P2PWait& wait, hipStream_t 
 // kRedThreads-th block column, then the wave butterflies and the wave sums in wave order — the
 // same fixed tree in both kernels (bit-identical).  1024 threads (four times the loads in
 // flight) measured no faster at 62.5k or 500k (profiles/r02_ab_red_threads.txt).
-#ifndef FREI_RED_THREADS
-#define FREI_RED_THREADS 256
-#endif
-constexpr int kRedThreads = FREI_RED_THREADS;
+constexpr int kRedThreads = 256;
 constexpr int kRedWaves = kRedThreads / 64;
 
 __global__ __launch_bounds__(kRedThreads) void reduce_kernel(const double* __restrict__ part,
@@ -2498,11 +2236,7 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
     const double T1 = sT[i];
     const double T2 = top ? T1 : sT[i + 1];
     const double p2 = top ? a.su.p_top2 : sP[i + 1];
-#ifdef FREI_UPD_NODT  // diagnostic ablation build
-    sdT[i] = 1e-3 * (Fb[0] - Fb[1]) + T2 * 1e-9 + p2 * 1e-20;
-#else
     sdT[i] = layer_dT(Fb, T1, T2, sP[i], p2, sLn[i], a.su.g, a.m_bar, a.alpha);
-#endif
   }
   __syncthreads();
   // T <- T - dT for every layer (untouched layers have dT = 0, Q6)
@@ -2547,11 +2281,9 @@ __global__ __launch_bounds__(256) void update_kernel(UpdateArgs a) {
     *a.iter = it + 1;
     if (all_conv && a.stop_on_conv) *a.conv = 1;
   }
-#ifndef FREI_UPD_NOSETUP  // diagnostic ablation build
   if (a.next_dir >= 0)
     setup_sweep(a.su, sT, sP, sTn, meta ? sSp : a.su.spec, meta ? sPm : a.su.pmeta,
                 meta ? sMm : a.su.mmr, a.next_dir, 0, ns, threadIdx.x, blockDim.x, nL, 0);
-#endif
 }
 
 // ---------------------------------------------------------------- reduce + update, fused
@@ -2609,9 +2341,6 @@ __device__ __forceinline__ void update_arrive(const UpdateArgs& a, int nU, int i
 template <int U = 1>
 __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, int h,
                                   double* sh) {
-#ifdef FREI_UPD_EMPTY  // diagnostic ablation build: launch floor
-  return;
-#endif
   TRACE_DECL;
   const int nL = a.su.n_layers;
   const bool on = lr < nL;
@@ -2668,11 +2397,7 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
     return;
   }
   // ---- this rank's sums, reduce_kernel's order (strided per thread, wave butterfly, waves)
-#ifdef FREI_UPD_NOSUM  // diagnostic ablation build
-  if (false) {
-#else
   if (k0 >= 0 || k1 >= 0) {
-#endif
     const double* pj[8];
     for (int j = 0; j < 8; ++j) {
       const int k = (j < 4) ? (k0 >= 0 ? k0 : k1) : (k1 >= 0 ? k1 : k0);
@@ -2735,10 +2460,8 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
   }
   __syncthreads();
   const long long t0 = wall_clock64();
-#ifndef FREI_P2P_NOPUSH   // diagnostic ablation build: no push (a one-rank run still completes)
   if (a.p2p.mbox && tid == 64 && k0 >= 0 && on)
     p2p_push_values(a.push, (int64_t)k0 * 4, tot, 4);
-#endif
   if (tid < 64) {
     // all ranks' sums in rank order (lanes 0..7), then dT of layers l, l + 1 (lanes 0, 1)
     double v = 0.0;
@@ -2765,11 +2488,7 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
       atomicAdd(a.p2p.wait_ticks, (unsigned long long)(wall_clock64() - t0));
     double d = 0.0;
     if (tid < 2 && kd >= 0) {
-#ifdef FREI_UPD_NODT  // diagnostic ablation build
-      d = 1e-3 * (F[0] - F[1]) + T2 * 1e-9 + p2 * 1e-20 + lnp * 0 + pre.dz * 0;
-#else
       d = layer_dT_post(F, pre);
-#endif
       sTn[li] = T1 - d;
     }
     if (tid == 0 && on) {
@@ -2808,7 +2527,6 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
   }
   TRACE_MARK(2);
   __syncthreads();   // sTn of layers l, l + 1
-#ifndef FREI_UPD_NOSETUP  // diagnostic ablation build
   if (kn >= 0 && tid >= 64 && on) {
     if (stage)
       setup_sweep(a.su, sTn, sP, sNodes, sSp, sPm, sMm, a.next_dir, kn, kn + 1, tid - 64,
@@ -2817,7 +2535,6 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
       setup_sweep(a.su, sTn, sP, sNodes, a.su.spec, a.su.pmeta, a.su.mmr, a.next_dir, kn,
                   kn + 1, tid - 64, kRedThreads - 64, nL, 0);
   }
-#endif
   TRACE_PUT(30);
 }
 
@@ -2827,21 +2544,15 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
 // on its converged path; *a.conv is read before the first, and it is only written by the last
 // layer to arrive, after every block has passed its second barrier — so both reads agree.
 __device__ __forceinline__ void update_shadow(const UpdateArgs& a) {
-#ifdef FREI_UPD_EMPTY
-  return;
-#endif
   if (!a.force && *a.conv) return;
   __syncthreads();
   __syncthreads();
   __syncthreads();
 }
 
-#ifndef FREI_UPD_BATCH
-#define FREI_UPD_BATCH 8
-#endif
 __global__ __launch_bounds__(kRedThreads) void update_fused_kernel(UpdateArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sh[];
-  update_fused_body<FREI_UPD_BATCH>(a, blockIdx.x, gridDim.x, threadIdx.x, 0, sh);
+  update_fused_body<8>(a, blockIdx.x, gridDim.x, threadIdx.x, 0, sh);
 }
 
 // Chained launch: workgroups [0, nU) run the previous sweep's fused update (u; with 8-wave
@@ -2916,7 +2627,7 @@ void launch_sweep_pipe_chain(int dir, int PF, const FastArgs& a, const UpdateArg
 
 // The one-lane form chained (contracted single table, step records formed in the block).
 template <int DIR, int PD, int PF>
-__global__ __launch_bounds__(kBlock, FREI_LB_WAVES) void sweep_fast_chain_kernel(
+__global__ __launch_bounds__(kBlock, 1) void sweep_fast_chain_kernel(
     FastArgs a, UpdateArgs u, const FastStepS* __restrict__ ss, double* __restrict__ Fu,
     double* __restrict__ Fd, double* __restrict__ part, double* __restrict__ dtaus) {
   static_assert(kRedThreads == kBlock, "update workgroups of the sweep's block size");
@@ -3219,41 +2930,15 @@ struct ContractBatchArgs {
   int64_t pitch, tab_stride;
 };
 
-#ifndef FREI_K7_WIDE
-#define FREI_K7_WIDE 1
-#endif
-#ifndef FREI_K7_NT
-#define FREI_K7_NT 0
-#endif
-#if FREI_K7_WIDE
 // 128 columns per wave, 16 B per lane per store: each store instruction writes one
 // atmosphere's 128 contiguous columns (1 KiB); the 16 x 128 D block goes through LDS in two
-// halves of 8 atmospheres (rows padded to 144 doubles: 1152 B = 128 B mod 256)
+// halves of 8 atmospheres (rows padded to 144 doubles: 1152 B = 128 B mod 256).  (64 columns
+// with 8-B stores, and non-temporal stores: measured slower, profiles/r04/c5/.)
 constexpr int kK7Cols = 128;
 constexpr int kK7Row = kK7Cols + 16;
 constexpr int kK7Rows = 8;
-#else
-constexpr int kK7Cols = 64;          // columns per wave (four 16-column MFMA tiles)
-constexpr int kK7Row = kK7Cols + 16; // LDS row pitch in doubles (640 B: 128 B mod 256)
-constexpr int kK7Rows = 16;
-#endif
 constexpr int kK7Tiles = kK7Cols / 16;
 typedef double dbl2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ void k7_store(double* p, double v) {
-#if FREI_K7_NT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
-__device__ __forceinline__ void k7_store(dbl2* p, dbl2 v) {
-#if FREI_K7_NT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
 
 template <int S>
 __global__ __launch_bounds__(256) void contract_batch_kernel(ContractBatchArgs a) {
@@ -3315,18 +3000,11 @@ __global__ __launch_bounds__(256) void contract_batch_kernel(ContractBatchArgs a
       __syncthreads();
       const int mlo = m0 + h * kK7Rows;
       const int mrows = max(0, min(kK7Rows, a.n_atm - mlo));
-#if FREI_K7_WIDE
       if (col0 + 2 * lane < ncol)
         for (int m = 0; m < mrows; ++m)
-          k7_store(reinterpret_cast<dbl2*>(a.eff + (int64_t)(mlo + m) * a.tab_stride + rowbase +
-                                           col0 + 2 * lane),
-                   *reinterpret_cast<const dbl2*>(my + m * kK7Row + 2 * lane));
-#else
-      if (col0 < ncol)
-        for (int m = 0; m < mrows; ++m)
-          k7_store(a.eff + (int64_t)(mlo + m) * a.tab_stride + rowbase + col0 + lane,
-                   my[m * kK7Row + lane]);
-#endif
+          *reinterpret_cast<dbl2*>(a.eff + (int64_t)(mlo + m) * a.tab_stride + rowbase + col0 +
+                                   2 * lane) =
+              *reinterpret_cast<const dbl2*>(my + m * kK7Row + 2 * lane);
       __syncthreads();   // the next half / atmosphere tile overwrites this wave's LDS block
     }
   }

@@ -305,6 +305,35 @@ bool lam2_blocks(const frei_ctx* c) {
   return (int64_t)c->nblocks * (c->n_atm > 1 ? c->n_atm : 1) >= kLam2MinBlocks;
 }
 
+// Staged partial sums (red_rows 2): the per-wave LDS tile plus one row per wave and the step
+// table within 48 KiB (deep atmospheres, above ~160 steps, do not fit).
+bool staged_sums_fit(int ns) {
+  return ((size_t)(kBlock / 64) * ns * 4 + (size_t)(kBlock / 64) * 2 * 4 * 72) * sizeof(double) +
+             (size_t)ns * sizeof(FastStepS) <= 48 * 1024;
+}
+// Prefetch depth of the one-lane sweep: below ~2 waves per SIMD (small per-GPU slices, e.g. 500k
+// lambda over 8 GPUs) a second layer in flight hides HBM latency; at full occupancy one suffices.
+// With one table (K3) and few blocks per CU, four steps in flight add the instruction-level
+// parallelism that occupancy cannot (FREI_DEPTH4_MAX_BLOCKS).
+int sweep_depth(const frei_ctx* c, int S_run) {
+  return c->prefetch_depth > 0 ? c->prefetch_depth
+         : (S_run == 1 && c->nblocks <= c->depth4_max_blocks) ? 4 : 2;
+}
+// Loads issued pf steps ahead (the contracted table only; 0: the coefficient block's depth;
+// prefetch_steps 2 with depth 1: one step per coefficient block, loads two steps ahead).
+int sweep_pf(const frei_ctx* c, bool eff, int S_run, int depth) {
+  return (eff && S_run == 1 && (depth >= 2 || c->prefetch_steps == 2)) ? c->prefetch_steps : 0;
+}
+// The two-wavelength sweep's requirements besides the contracted NaN-free table, one lane per
+// wavelength, global step records and no chained launch: an even slice, enough one-lane blocks
+// (or FREI_LAM2=1), a depth-2 coefficient block loading at most two steps ahead, and the staged
+// partial sums.  run_sweep (fast_form), frei_ctx_path and the batched step-table choice
+// (build_meta) all decide by it.
+bool lam2_static(const frei_ctx* c, int depth, int pf) {
+  return c->lam2 != 0 && c->nlam % 2 == 0 && (c->lam2 > 0 || lam2_blocks(c)) && depth == 2 &&
+         pf <= 2 && c->red_stage && staged_sums_fit(c->nL - 1);
+}
+
 template <typename Lap>
 int build_contracted(frei_ctx* c, bool shared_fast, Lap&& lap) {
   const int nL = c->nL, S = c->S;
@@ -512,7 +541,9 @@ int build_meta(frei_ctx* c) {
   }
   // batched launches with many blocks in all take the two-wavelength sweep, which reads the
   // step records from global memory (C5, 32 x 100k lambda: -9 % per step, profiles/r04/c5/)
-  const bool lam2_batch = c->n_atm > 1 && c->lam2 != 0 && c->nlam % 2 == 0 && lam2_blocks(c);
+  // (a batched context always has the contracted table without NaN, or fails in build_contracted)
+  const int bdepth = sweep_depth(c, 1);
+  const bool lam2_batch = c->n_atm > 1 && lam2_static(c, bdepth, sweep_pf(c, true, 1, bdepth));
   const bool small = c->nblocks <= c->shared_max_blocks && !lam2_batch;
   // the LDS-staged step table plus one partial-sum row per wave must leave room for several
   // blocks per CU (deep atmospheres: > ~260 layers read the step table from global memory)
@@ -546,7 +577,7 @@ AtmStride atm_stride(frei_ctx* c);
 
 // Lanes per wavelength of the sweep: the grouped-lane kernel (2 or 4 lanes) when the slice
 // leaves about one wave per SIMD or less (contracted table, LDS step table), else 1.
-int group_lanes(frei_ctx* c) {
+int group_lanes(const frei_ctx* c) {
   if (!(c->fast && c->eff && c->shared)) return 1;
   if (c->group_q > 0) return c->group_q;
   const int64_t blocks = (int64_t)c->nblocks * c->n_atm;   // 256-wavelength blocks
@@ -557,7 +588,7 @@ int group_lanes(frei_ctx* c) {
 
 // Consumers per block of the producer/consumer sweep (0: not used).  Contracted table and the
 // FastStepS records (the LDS-step-table path); the block's LDS must fit the device.
-int pipe_consumers(frei_ctx* c) {
+int pipe_consumers(const frei_ctx* c) {
   if (!(c->fast && c->eff && c->shared) || c->pipe_nc == 0) return 0;
   int nc = c->pipe_nc;
   if (nc < 0) {   // by slice size: one 256-wavelength block per CU or fewer
@@ -655,6 +686,16 @@ void rotate_T(frei_ctx* c, double* out) {
 }
 double* free_T(frei_ctx* c, const double* busy) { return c->d_T_alt != busy ? c->d_T_alt : c->d_T3; }
 
+// Drop a deferred update that will never run (an error part-way through a run).  The sweep that
+// deferred it already made its output buffer the current temperatures, filled with kPoisonT
+// ("not published"), so the current temperatures go back to that update's input: a later sweep
+// or read that skips frei_state_init sees the last published temperatures, not poison.
+void drop_pending(frei_ctx* c) {
+  if (!c->has_pend) return;
+  c->has_pend = false;
+  rotate_T(c, c->pend.su.T);
+}
+
 // reduce + update fused into one launch: one atmosphere, exchange local or P2P (RCCL and the
 // host hook need the rank's sums in memory between the two kernels)
 bool fused_ok(frei_ctx* c) {
@@ -705,6 +746,38 @@ uint64_t arg_hash(uint64_t h, const T& x) {
   const unsigned char* b = reinterpret_cast<const unsigned char*>(&x);
   for (size_t i = 0; i < sizeof(T); ++i) h = (h ^ b[i]) * 1099511628211ull;
   return h;
+}
+
+// The sweep form run_sweep launches for the contracted / per-species tables (c->fast), in one
+// place, so that frei_ctx_path reports what runs.  merge: the launch also runs a deferred update.
+struct FastForm {
+  int S_run, depth, pf, Q, NW, NC, red_rows;
+  bool nan_check, lam2;
+};
+FastForm fast_form(const frei_ctx* c, bool merge) {
+  FastForm m{};
+  const int ns = c->nL - 1;
+  m.S_run = c->eff ? 1 : c->S;
+  // per-row partials while the one-lane sweep's LDS stays within 48 KiB (3+ blocks per CU)
+  m.red_rows = c->red_rows &&
+               (size_t)16 * ns * 4 * sizeof(double) + (size_t)ns * sizeof(FastStepS) <= 48 * 1024;
+  m.depth = sweep_depth(c, m.S_run);
+  m.pf = sweep_pf(c, c->eff != 0, m.S_run, m.depth);
+  m.nan_check = false;
+  for (int q = 0; q < c->S; ++q) m.nan_check = m.nan_check || c->sp[q].has_nan;
+  m.Q = group_lanes(c);
+  // staged partial sums (mode 2): the one-lane sweep with two steps in flight, and the
+  // grouped-lane sweep (two groups in flight)
+  if ((m.Q > 1 || m.depth == 2 || (m.depth == 1 && m.pf == 2)) && c->red_stage &&
+      staged_sums_fit(ns))
+    m.red_rows = 2;
+  m.NW = c->group_waves;
+  m.NC = pipe_consumers(c);
+  // two wavelengths per lane: the one-lane contracted sweep on slices that need more than
+  // about one round of one-lane blocks (1280 resident at five waves per SIMD on 256 CUs)
+  m.lam2 = c->eff && m.S_run == 1 && !c->shared && !m.nan_check && m.Q == 1 && m.NC == 0 &&
+           !merge && m.red_rows == 2 && lam2_static(c, m.depth, m.pf);
+  return m;
 }
 
 // One sweep: K1 -> fused reduce + update (+ next setup; P2P exchange inside), or K1 ->
@@ -768,7 +841,8 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
     f.sig = c->d_sig;
     f.wtr = c->d_wtr;
     f.ftoa = c->d_ftoa;
-    const int S_run = c->eff ? 1 : c->S;
+    const FastForm m = fast_form(c, merge);
+    const int S_run = m.S_run;
     for (int q = 0; q < kMaxFastS; ++q) f.tab[q] = q < c->S ? c->sp[q].d_tab : nullptr;
     if (c->eff) f.tab[0] = c->d_eff;
     f.steps = c->d_fsteps;
@@ -792,38 +866,11 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
     }
     if (defer_own) f.poison = T_next;
     if (f.rec_on) f.rec = setup_args(c);   // T of this sweep: c->d_T now
-    // per-row partials while the one-lane sweep's LDS stays within 48 KiB (3+ blocks per CU)
-    f.red_rows = c->red_rows &&
-                 (size_t)16 * ns * 4 * sizeof(double) + (size_t)ns * sizeof(FastStepS) <=
-                     48 * 1024;
-    // Prefetch depth: below ~2 waves per SIMD (small per-GPU slices, e.g. 500k lambda over
-    // 8 GPUs) a second layer in flight hides HBM latency; at full occupancy one suffices.
-    // With one table (K3) and few blocks per CU, four steps in flight add the
-    // instruction-level parallelism that occupancy cannot (FREI_DEPTH4_MAX_BLOCKS).
-    const int depth = c->prefetch_depth > 0 ? c->prefetch_depth
-                      : (S_run == 1 && c->nblocks <= c->depth4_max_blocks) ? 4 : 2;
-    // loads issued pf steps ahead (the contracted table only; 0: the coefficient block's depth)
-    // (prefetch_steps 2 with depth 1: one step per coefficient block, loads two steps ahead)
-    const int pf = (c->eff && S_run == 1 && (depth >= 2 || c->prefetch_steps == 2))
-                       ? c->prefetch_steps : 0;
-    bool nan_check = false;
-    for (int q = 0; q < c->S; ++q) nan_check = nan_check || c->sp[q].has_nan;
-    const int Q = group_lanes(c);
-    // staged partial sums (mode 2): the one-lane sweep with two steps in flight, and the
-    // grouped-lane sweep (two groups in flight)
-    if ((Q > 1 || depth == 2 || (depth == 1 && pf == 2)) && c->red_stage &&
-        ((size_t)(kBlock / 64) * ns * 4 + (size_t)(kBlock / 64) * 2 * 4 * 72) * sizeof(double) +
-                (size_t)ns * sizeof(FastStepS) <= 48 * 1024)
-      f.red_rows = 2;
-    const int NW = c->group_waves;
+    f.red_rows = m.red_rows;
+    const int depth = m.depth, pf = m.pf, Q = m.Q, NW = m.NW, NC = m.NC;
+    const bool nan_check = m.nan_check, lam2 = m.lam2;
     if (Q > 1) nb_run = (int)((c->nlam + 64 * NW / Q - 1) / (64 * NW / Q));
-    const int NC = pipe_consumers(c);
     if (NC > 0) nb_run = (int)((c->nlam + 64 * NC - 1) / (64 * NC));
-    // two wavelengths per lane: the one-lane contracted sweep on slices that need more than
-    // about one round of one-lane blocks (1280 resident at five waves per SIMD on 256 CUs)
-    const bool lam2 = c->lam2 != 0 && c->eff && S_run == 1 && !c->shared && !nan_check &&
-                      Q == 1 && NC == 0 && !merge && depth == 2 && pf <= 2 && f.red_rows == 2 &&
-                      c->nlam % 2 == 0 && (c->lam2 > 0 || lam2_blocks(c));
     if (lam2) nb_run = (int)((c->nlam + 2 * kBlock - 1) / (2 * kBlock));
     if (c->keys) {
       uint64_t h = arg_hash(1469598103934665603ull, f);
@@ -1091,7 +1138,7 @@ int check_comm(frei_ctx* c) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->chain_checked = c->n_chained;
   if (chain && c->h_err[0]) {   // reported once: rearm it so later runs are not failed by it
-    c->has_pend = false;
+    drop_pending(c);
     c->h_err[0] = 0;
     HIP_TRY(hipMemsetAsync(c->d_chain_err, 0, sizeof(int), c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1602,11 +1649,12 @@ int frei_state_init(frei_ctx* c, const double* T_init) {
 
 static int iterate_steps(frei_ctx* c, int n, int nzc, double thr, double alpha, bool stop);
 
-// An error part-way leaves no update deferred: a later frei_state_init + sweep must not flush a
-// stale one over the freshly uploaded temperatures.
+// An error part-way leaves no update deferred (drop_pending): a later frei_state_init + sweep
+// must not flush a stale one over the freshly uploaded temperatures, and a read without
+// frei_state_init sees the deferred update's input temperatures, not its poisoned output.
 static int iterate_direct(frei_ctx* c, int n, int nzc, double thr, double alpha, bool stop) {
   const int rc = iterate_steps(c, n, nzc, thr, alpha, stop);
-  if (rc != 0) c->has_pend = false;
+  if (rc != 0) drop_pending(c);
   return rc;
 }
 
@@ -2124,13 +2172,11 @@ int frei_ctx_path(frei_ctx* c, int* flags) {
   TRY(build_meta(c));
   int nan = 0;
   for (const auto& q : c->sp) nan = nan || q.has_nan;
-  const int Q = group_lanes(c);
-  const int NC = pipe_consumers(c);
-  // (the sweep itself also requires a depth-2 coefficient block with staged sums: the defaults)
-  const bool lam2 = c->lam2 != 0 && c->fast && c->eff && !c->shared && Q == 1 && NC == 0 &&
-                    c->nlam % 2 == 0 && (c->lam2 > 0 || lam2_blocks(c)) &&
-                    c->prefetch_depth != 1 && c->prefetch_depth < 4 && c->prefetch_steps <= 2 &&
-                    c->red_stage;
+  // the form run_sweep launches: a loop's sweeps after the first merge a deferred update when
+  // chained launches apply
+  const FastForm m = fast_form(c, chain_ready(c));
+  const int Q = m.Q, NC = m.NC;
+  const bool lam2 = c->fast && m.lam2;
   *flags = (c->fast ? 1 : 0) | (c->fast && c->shared ? 2 : 0) | (c->eff ? 4 : 0) |
            (nan ? 8 : 0) | (NC == 0 && Q == 2 ? 16 : 0) | (NC == 0 && Q == 4 ? 32 : 0) |
            (NC << 6) | (lam2 ? 512 : 0);

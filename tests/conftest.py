@@ -36,11 +36,10 @@ def _provenance(session, exitstatus):
             "pytest_args": [str(a) for a in session.config.invocation_params.args],
             "exitstatus": int(exitstatus), "outcomes": dict(_OUTCOMES),
             "tree_hash": digest, "tree_files": n_files}
-    try:
-        with open(os.path.join(ROOT, "frei_amd/libfrei_hip.so.stamp")) as f:
-            prov["lib_source_hash"] = f.read().strip()
-    except OSError:
-        prov["lib_source_hash"] = None
+    from frei_amd.build import read_stamp, source_hash
+    prov["lib_source_hash"], compiler = read_stamp()
+    prov["lib_compiler"] = (compiler or "").splitlines()[:2]
+    prov["lib_matches_tree"] = prov["lib_source_hash"] == source_hash()
     return prov
 
 
