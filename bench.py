@@ -53,8 +53,13 @@ def parse():
                     help="max T-P iterations for the iterations-to-radiative-equilibrium run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-lam", type=int, default=50_000)
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
-                    help="threads of the all-cores CPU leg (1 = skip it)")
+    ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
+                    help="worker processes of the all-cores CPU leg (1 = skip it; the GPU box "
+                         "grants a 16-CPU share)")
+    ap.add_argument("--cpu-sharded-lam", type=int, default=500_000,
+                    help="wavelengths of the all-cores CPU leg's sample")
+    ap.add_argument("--no-provider", action="store_true",
+                    help="skip the chemistry-provider (chemistry=) measurement")
     ap.add_argument("--no-binning", action="store_true",
                     help="skip the K6 opacity-binning measurement (rank 0)")
     ap.add_argument("--binning-reps", type=int, default=5)
@@ -138,36 +143,92 @@ def cpu_baseline(w, n_sample, steps=1):
     return updates / dt, dt
 
 
-def cpu_baseline_threads(w, n_per_thread, threads, steps=1):
-    """The oracle λ-sharded over `threads` host threads (SURVEY.md §8(d)'s optional all-cores
-    variant): each thread runs the same path on its own disjoint wavelength sample of
-    `n_per_thread` (NumPy's ufuncs release the GIL on these array sizes).  Timing only — the
-    shards do not exchange their bolometric sums, so their temperatures are not the unsharded
-    run's — the same arithmetic per update as cpu_baseline.  Threads, not processes: this
-    process already holds a GPU context."""
-    from concurrent.futures import ThreadPoolExecutor
-    from oracle import frei_oracle as O
+def cpu_baseline_sharded(w, n_lam, workers, steps=1):
+    """The oracle λ-sharded over `workers` processes (SURVEY.md §8(d)'s all-cores variant):
+    oracle/sharded.py runs the unchanged oracle on contiguous slices of an evenly strided
+    `n_lam`-wavelength sample and exchanges the four bolometric partial sums per layer through the
+    coordinator, so every slice steps the same temperatures as the one-process run.  The worker
+    processes are spawned (they never touch the GPU) before the clock starts; the timed region is
+    the run itself, exchanges included."""
+    from oracle.sharded import ShardedOracle
     lam = w["lam"]
-    idx_all = np.linspace(0, lam.size - 1, n_per_thread * threads).round().astype(int)
-    jobs = []
-    for t in range(threads):
-        idx = idx_all[t::threads]
-        tabs = {n: O.Table(O.SeparableValues(w["base"][s][idx], w["fp"][s], w["fT"][s]),
-                           w["p"], w["T_nodes"]) for s, n in enumerate(w["names"])}
-        jobs.append((tabs, lam[idx], O.F_TOA(lam[idx])))
-
-    def one(job):
-        tabs, lam_s, Ft = job
-        O.emission_spectrum(tabs, w["T0"], w["p"], lam_s, Ft, 2478.6519476149147,
-                            4.0142926168559996e-24, 1, n_timesteps=steps,
-                            n_zero_crossings=10 ** 9, convergence_dT=-1.0, mmr=w["mmr"])
-
-    with ThreadPoolExecutor(threads) as ex:
+    idx = np.linspace(0, lam.size - 1, n_lam).round().astype(int)
+    tables = {n: (w["base"][s][idx], w["fp"][s], w["fT"][s], w["T_nodes"])
+              for s, n in enumerate(w["names"])}
+    from oracle import frei_oracle as O
+    with ShardedOracle(tables, lam[idx], w["p"], w["T0"], O.F_TOA(lam[idx]), 2478.6519476149147,
+                       4.0142926168559996e-24, mmr=w["mmr"], n_workers=workers) as so:
+        so.emission_spectrum(n_timesteps=1, n_zero_crossings=10 ** 9,
+                             convergence_dT=-1.0)          # untimed: workers import, warm up
         t0 = time.perf_counter()
-        list(ex.map(one, jobs))
+        so.emission_spectrum(n_timesteps=steps, n_zero_crossings=10 ** 9, convergence_dT=-1.0)
         dt = time.perf_counter() - t0
-    updates = (2 * steps + 1) * (w["p"].size - 1) * n_per_thread * threads
+    updates = (2 * steps + 1) * (w["p"].size - 1) * n_lam
     return updates / dt, dt
+
+
+# SURVEY.md §6: the reference itself (imported in the build container, 1 core), whole
+# emission_spectrum path, 60 layers x 500k lambda, one species: 62.3 s for 3 sweeps
+REFERENCE_MEASURED = {"value": 1.42e6, "unit": "updates/s", "cores": 1, "species": 1,
+                      "source": "SURVEY.md §6 (frei's own Grid.emission_spectrum in the build "
+                                "container, 60 x 500k lambda, 1 species, 1 core of a Xeon)"}
+
+
+def provider_leg(a, d, w, tabs):
+    """The drop-in's chemistry path (frei's chemistry passed as chemistry=): a
+    T-dependent provider on the reference's signature (frei_amd.workloads.c3_provider, the
+    FastChem stand-in) drives the C3 run to radiative equilibrium.  Every sweep: the layers' T
+    read back (8 B per layer), the provider called on them as kappa calls it
+    (opacity.py:246-248), the mixing ratios uploaded, the per-species sweep and its update.
+    Reports iterations/s and where a sweep's wall time goes (sweep kernel vs the rest: update
+    kernel, T readback, provider call, mixing-ratio upload, launch and synchronisation)."""
+    from frei_amd.engine import Engine
+    from frei_amd.workloads import c3_provider
+    prov = c3_provider(w)
+    n_calls = [0]
+
+    def counted(*args, **kw):
+        n_calls[0] += 1
+        return prov(*args, **kw)
+    pe = Engine(w["lam"], w["p"], tabs, chemistry=counted, device=d.local)
+    try:
+        path = pe.path()
+        pe.run(w["T0"], n_timesteps=2, n_zero_crossings=2, convergence_dT=3.0, alpha=1.0,
+               want_dtaus=False)                                      # warm-up
+        n0 = n_calls[0]
+        t0 = time.perf_counter()
+        out = pe.run(w["T0"], n_timesteps=a.rad_eq_max, n_zero_crossings=2, convergence_dT=3.0,
+                     alpha=1.0, want_dtaus=False)
+        wall = time.perf_counter() - t0
+        calls = n_calls[0] - n0
+        pe.timing(True)                                               # the same run, timed
+        t2 = time.perf_counter()
+        pe.run(w["T0"], n_timesteps=a.rad_eq_max, n_zero_crossings=2, convergence_dT=3.0,
+               alpha=1.0, want_dtaus=False)
+        wall_t = time.perf_counter() - t2
+        ms, n_sw = pe.timing_read()
+        pe.timing(False)
+        # the provider alone, on one sweep's layer temperatures (host side)
+        T = out["final_T"]
+        t4 = time.perf_counter()
+        for _ in range(20):
+            prov(T, w["p"], w["names"], m_bar=4.0142926168559996e-24)
+        prov_ms = (time.perf_counter() - t4) / 20 * 1e3
+    finally:
+        pe.close()
+    it = out["n_iter"]
+    n_sweeps = 2 * it + 1
+    return {"workload": f"C3 60 x {a.n_lam} lambda x {len(w['names'])} species to radiative "
+                        "equilibrium, mixing ratios from a T-dependent provider (chemistry=)",
+            "path": path, "iterations": it, "wall_s": wall, "iters_per_s": it / wall,
+            "sweeps": n_sweeps, "provider_calls": calls,
+            "ms_per_sweep": wall / n_sweeps * 1e3,
+            "sweep_kernel_ms": ms / max(n_sw, 1),
+            "rest_ms_per_sweep": (wall_t * 1e3 - ms) / max(n_sw, 1),
+            "provider_call_ms": prov_ms,
+            "note": "rest_ms_per_sweep: the timed run's wall time per sweep outside the sweep "
+                    "kernel (HIP events): update kernel, T readback, the provider call, the "
+                    "mixing-ratio upload, launches and stream synchronisation"}
 
 
 def binning_leg(a, device, cpu=True):
@@ -571,15 +632,20 @@ def main():
                          f"{os.cpu_count()} host CPUs), {nL} layers x {min(a.cpu_lam, n_lam)} "
                          f"lambda (evenly strided sample of the same grid), {S} species, 1 T-P "
                          f"iteration + final emit, {dt:.1f} s"}
-        if a.cpu_threads > 1:
-            n_t = max(1, min(a.cpu_lam, n_lam) // 4)
-            rate_t, dt_t = cpu_baseline_threads(w, n_t, a.cpu_threads)
+        cpu["reference_measured"] = dict(REFERENCE_MEASURED,
+                                         port_over_reference=rate / REFERENCE_MEASURED["value"],
+                                         note="the port's figure is 8 species (K3 not used: "
+                                              "the oracle sums every species per update)")
+        if a.cpu_workers > 1:
+            n_s = min(a.cpu_sharded_lam, n_lam)
+            rate_t, dt_t = cpu_baseline_sharded(w, n_s, a.cpu_workers)
             cpu["all_cores"] = {
-                "value": rate_t, "unit": "updates/s", "cores": a.cpu_threads,
+                "value": rate_t, "unit": "updates/s", "cores": a.cpu_workers,
                 "speedup_over_1_core": rate_t / rate,
-                "sample": f"the same oracle path lambda-sharded over {a.cpu_threads} threads "
-                          f"({n_t} lambda each, disjoint strided samples, no exchange of "
-                          f"bolometric sums between shards: timing only), {dt_t:.1f} s"}
+                "sample": f"the same oracle path in {a.cpu_workers} worker processes on "
+                          f"contiguous slices of a {n_s}-lambda strided sample, bolometric sums "
+                          f"exchanged per layer (oracle/sharded.py: the temperatures of the "
+                          f"one-process run), 1 T-P iteration + final emit, {dt_t:.1f} s"}
     eng.close()
 
     # ---- T-dependent chemistry (mmr tabulated on (T, p), re-interpolated on the device before
@@ -608,6 +674,10 @@ def main():
                            "iters_per_s": cout["n_iter"] / (t5 - t4)},
                 "note": "synthetic T-dependent mixing ratios (frei_amd.workloads.c3_chemistry) "
                         "re-interpolated per layer before every sweep; per-species sweep (no K3)"}
+
+    provider = None
+    if d.world == 1 and not a.no_provider and not a.force_comm:
+        provider = provider_leg(a, d, w, tabs)
 
     # PMC traffic / VALU of the same workload (separate rocprofv3 --pmc passes, committed)
     traffic, traffic_src, valu = None, None, None
@@ -694,6 +764,7 @@ def main():
                                      "loop"}},
             "per_species": per_species,
             "chemistry": chem,
+            "provider": provider,
             "cpu_baseline": cpu,
             "k6_binning": binning,
             "c5_batched": c5,

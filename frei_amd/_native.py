@@ -48,6 +48,7 @@ SIGNATURES = {
     "frei_set_chemistry": (ctypes.c_int, [_vp, _dp, _dp, ctypes.c_int, _dp, ctypes.c_int]),
     "frei_set_fluxes": (ctypes.c_int, [_vp, _dp, _dp]),
     "frei_get_fluxes": (ctypes.c_int, [_vp, _dp, _dp]),
+    "frei_get_spectrum": (ctypes.c_int, [_vp, _dp]),
     "frei_set_temperatures": (ctypes.c_int, [_vp, _dp]),
     "frei_get_temperatures": (ctypes.c_int, [_vp, _dp]),
     "frei_sweep": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double, _dp, _dp, _dp]),

@@ -142,6 +142,7 @@ struct frei_ctx {
   std::vector<Species> sp;
   std::vector<double> mmr;
   bool meta_dirty = true;
+  bool mmr_dirty = false;               // only the mixing ratios changed (per-sweep provider)
   int fast = 1;
   SpecMeta* d_smeta = nullptr;
   PMeta* d_pmeta = nullptr;
@@ -454,7 +455,13 @@ double now_ms() {
 }
 
 int build_meta(frei_ctx* c) {
-  if (!c->meta_dirty) return 0;
+  if (!c->meta_dirty) {
+    if (c->mmr_dirty) {   // new mixing ratios only: up on the stream, ahead of the next sweep
+      TRY(h2d(c->d_mmr, c->mmr.data(), c->mmr.size(), c->stream));
+      c->mmr_dirty = false;
+    }
+    return 0;
+  }
   if (!c->grid_set) return fail("frei_set_grid must be called before using tables");
   double t_prev = now_ms();
   auto lap = [&](int k) {   // frei_setup_timing phases (host wall clock, stream synced)
@@ -570,6 +577,7 @@ int build_meta(frei_ctx* c) {
   TRY(build_contracted(c, fast && shared, lap));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->meta_dirty = false;
+  c->mmr_dirty = false;
   return 0;
 }
 
@@ -1474,8 +1482,16 @@ int frei_set_table_binned(frei_ctx* c, int s, frei_xsec* x, int mode, const doub
 
 int frei_set_mmr(frei_ctx* c, const double* mmr) {
   if (!c || !mmr) return fail("null argument");
-  c->mmr.assign(mmr, mmr + (size_t)c->S * c->nL * c->n_atm);
-  c->meta_dirty = true;
+  const size_t n = (size_t)c->S * c->nL * c->n_atm;
+  // A chemistry provider evaluated between sweeps (T-dependent, frei_amd Engine) sets new mixing
+  // ratios before every sweep.  When the metadata is built and the sweep sums the species itself
+  // (no contraction K3 formed from the old ratios), nothing else depends on them: they only go up
+  // to the device before the next sweep forms its step records — not a metadata rebuild (bracket
+  // searches, uploads and stream synchronizations) per sweep.
+  const bool light = !c->meta_dirty && !c->eff && c->mmr.size() == n && c->d_mmr != nullptr;
+  c->mmr.assign(mmr, mmr + n);
+  if (light) c->mmr_dirty = true;
+  else c->meta_dirty = true;
   return 0;
 }
 
@@ -1572,6 +1588,16 @@ int frei_get_fluxes(frei_ctx* c, double* up, double* down) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (up) HIP_TRY(hipMemcpy(up, c->d_Fu, F * sizeof(double), hipMemcpyDeviceToHost));
   if (down) HIP_TRY(hipMemcpy(down, c->d_Fd, F * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int frei_get_spectrum(frei_ctx* c, double* spec) {
+  if (!c || !spec) return fail("null argument");
+  if (c->n_atm > 1) return fail("frei_get_spectrum is per atmosphere: use frei_run_batch");
+  TRY(set_device(c));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(spec, c->d_Fu + (size_t)(c->nL - 1) * c->nlam, c->nlam * sizeof(double),
+                    hipMemcpyDeviceToHost));
   return 0;
 }
 

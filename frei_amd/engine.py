@@ -268,6 +268,12 @@ class Engine:
         N.check(N.lib().frei_get_fluxes(self._ctx, N.dptr(up), N.dptr(down)))
         return up, down
 
+    def get_spectrum(self):
+        """The emergent spectrum F_up[-1] (core.py:335-338), one row read back."""
+        spec = np.empty(self.n_lam)
+        N.check(N.lib().frei_get_spectrum(self._ctx, N.dptr(spec)))
+        return spec
+
     def set_temperatures(self, T):
         N.check(N.lib().frei_set_temperatures(self._ctx, N.dptr(N.f64(T))))
 
@@ -346,8 +352,7 @@ class Engine:
                 break
         self._provider_step(T)
         _, _, dtaus = self.sweep(EMIT, alpha=1.0, want_dtaus=want_dtaus)   # Q7: alpha = 1
-        up, _ = self.get_fluxes()
-        return dict(spectrum=up[-1].copy(), final_T=self.get_temperatures(),
+        return dict(spectrum=self.get_spectrum(), final_T=self.get_temperatures(),
                     temp_hist=np.hstack(hists) if hists else np.empty((nL, 0)),
                     dtaus=dtaus, n_iter=it)
 

@@ -73,6 +73,24 @@ def c3_chemistry(w, n_T=14, n_p=9):
     return ChemistryTable(vals, cT, cp)
 
 
+def c3_provider(w):
+    """A T-dependent chemistry *provider* for the C3 species on the reference's chemistry
+    signature, ``chemistry(temperatures, pressures, species, return_vmr=False, m_bar=...)``
+    (frei/chemistry.py:114-116; pressures in bar): c3_chemistry's law evaluated at the query
+    points.  It stands in for FastChem on the path the drop-in takes (``chemistry=``, evaluated
+    on the host between sweeps); FastChem itself is third-party and absent."""
+    med = {n: float(np.median(w["mmr"][s])) for s, n in enumerate(w["names"])}
+    sign = {n: (-1) ** s for s, n in enumerate(w["names"])}
+
+    def chemistry(temperatures, pressures, species, return_vmr=False, m_bar=None):
+        T = np.atleast_1d(np.asarray(getattr(temperatures, "value", temperatures), dtype=float))
+        p = np.atleast_1d(np.asarray(getattr(pressures, "value", pressures), dtype=float))
+        x = np.tanh((T - 1500.0) / 400.0) + 0.05 * np.log10(p)
+        mmr = {n: med[n] * 10 ** (0.5 * sign[n] * x) for n in species}
+        return (mmr, dict(mmr)) if return_vmr else mmr
+    return chemistry
+
+
 def bytes_per_update(n_species, write_dtau=False, live_only=False):
     """Algorithmic HBM bytes per (layer, wavelength) flux update:
     stale opposite-stream read 8 + two flux writes 16 + two T-bracket rows per species.

@@ -124,6 +124,10 @@ int frei_set_chemistry(frei_ctx* ctx, const double* values, const double* T_node
 /* Flux state [n_layers][n_lam] (this slice), caller layout row-major. */
 int frei_set_fluxes(frei_ctx* ctx, const double* up, const double* down);
 int frei_get_fluxes(frei_ctx* ctx, double* up, double* down);
+/* The emergent spectrum F_up[n_layers - 1] of this slice (n_lam values): the row the reference's
+ * Grid returns as Spectrum1D(flux=fluxes_up[-1]) (frei/core.py:335-338), without reading back
+ * the whole flux state. */
+int frei_get_spectrum(frei_ctx* ctx, double* spectrum);
 int frei_set_temperatures(frei_ctx* ctx, const double* T);
 int frei_get_temperatures(frei_ctx* ctx, double* T);
 

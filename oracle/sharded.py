@@ -1,4 +1,5 @@
-"""The CPU oracle at BASELINE sizes — TEST INFRASTRUCTURE (a checker, never product code).
+"""The CPU oracle at BASELINE sizes — TEST INFRASTRUCTURE (a checker and bench.py's all-cores
+CPU baseline; never imported by the product, frei_amd).
 
 ``oracle.frei_oracle.emission_spectrum`` is single-threaded NumPy: 60 layers x 500k λ x 8
 species takes about a minute per sweep-triple on one core.  Within a sweep every wavelength is
@@ -37,7 +38,6 @@ def _trapz_weights(lam_cm):
 
 def _worker(conn, spec):
     from oracle import frei_oracle as O
-    from tests.parity import perturbed_exp
     lo, hi = spec["lo"], spec["hi"]
     lam = spec["lam"]
     tabs = {n: O.Table(O.SeparableValues(b, fp, fT), spec["p"], spec["T_nodes"][n])
@@ -54,6 +54,8 @@ def _worker(conn, spec):
                 conn.send(("part", np.array([np.sum(w * F2u), np.sum(w * F2d),
                                              np.sum(w * F1u), np.sum(w * F1d)])))
                 return conn.recv()
+            if perturb:   # the one-ulp floor: tests only
+                from tests.parity import perturbed_exp
             with perturbed_exp() if perturb else nullcontext():
                 with np.errstate(over="ignore", divide="ignore", invalid="ignore"):
                     out = O.emission_spectrum(tabs, spec["T0"], spec["p"], lam, spec["F_toa"],

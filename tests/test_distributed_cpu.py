@@ -127,10 +127,10 @@ def test_pointwise_trapz_weights_equal_np_trapz():
 
 
 def test_sharded_oracle_matches_one_process_oracle():
-    """tests/sharded_oracle.py (the checker of the full-size GPU parity tests) against the
+    """oracle/sharded.py (the checker of the full-size GPU parity tests) against the
     one-process oracle: same iterations, T within 1e-12, spectrum and fluxes within 1e-10."""
     from tests.parity import rel, row_normwise
-    from tests.sharded_oracle import ShardedOracle
+    from oracle.sharded import ShardedOracle
     rng = np.random.default_rng(8)
     lam, _, _ = O.wavelength_grid(0.5, 10, 1501)
     p = O.pressure_grid(16, -6, np.log10(200))

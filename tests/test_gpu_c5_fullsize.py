@@ -6,7 +6,7 @@ contraction per atmosphere on fp64 MFMA (K7), sweeps over (λ block, atmosphere)
 corners of that grid — T_ref 1000 / 2400 K, log g 2.5 / 4, [M/H] -1 / +1 — run batched at full
 size with bench.py's tables (c5_leg), a fixed 3 T-P iterations plus the final emit, and every
 atmosphere is compared with the oracle run on that atmosphere alone (the reference's per-Grid
-loop, core.py:233-338), λ-sharded over worker processes (tests/sharded_oracle.py).  Criterion:
+loop, core.py:233-338), λ-sharded over worker processes (oracle/sharded.py).  Criterion:
 tests/parity.py assert_grid_parity (1e-10, or twice the one-ulp floor of the reference
 algorithm measured on the same inputs), T within 1e-10; the errors go to the parity log.
 """
@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 from tests.parity import assert_grid_parity, grid_floor
-from tests.sharded_oracle import ShardedOracle
+from oracle.sharded import ShardedOracle
 
 pytestmark = pytest.mark.gpu
 

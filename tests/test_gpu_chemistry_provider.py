@@ -143,6 +143,7 @@ def test_provider_radiative_equilibrium_at_1e10_outright(fa):
     eng = grid.engine()
     assert eng.provider is prov and not eng.path()["contracted"]
     up, down = eng.get_fluxes()
+    assert np.array_equal(eng.get_spectrum(), up[-1])      # frei_get_spectrum: one row
 
     def run(provider):
         return O.emission_spectrum(tabs_o, T0, p, lam, O.F_TOA(lam), G_J, M_BAR, 1,

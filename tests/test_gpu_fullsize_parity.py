@@ -6,7 +6,7 @@
 - C2: 60 layers x 100,000 λ, H2O + CO, T nodes = the Grid's initial temperatures (the
   reference's own table layout: n_T = n_p = 60, descending), three T-P iterations.
 
-The oracle runs on wavelength slices in worker processes (tests/sharded_oracle.py; the
+The oracle runs on wavelength slices in worker processes (oracle/sharded.py; the
 bolometric sums are combined in slice order), with lazily built separable tables.  Criterion
 (tests/parity.py assert_grid_parity): emergent spectrum elementwise and F_up / F_down
 row-normwise within 1e-10, or twice the one-ulp floor of the reference algorithm on these very
@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from tests.parity import assert_grid_parity, grid_floor, row_normwise
-from tests.sharded_oracle import ShardedOracle
+from oracle.sharded import ShardedOracle
 
 pytestmark = pytest.mark.gpu
 

@@ -7,7 +7,7 @@ second half is the reference's T–P loop run to its own convergence test (core.
 as bench.py's ``rad_eq`` leg runs it (n_timesteps=200, n_zero_crossings=2, convergence_dT=3 K).
 
 The oracle runs the same loop on wavelength slices in worker processes
-(tests/sharded_oracle.py: bolometric sums combined in slice order, so every slice takes the same
+(oracle/sharded.py: bolometric sums combined in slice order, so every slice takes the same
 convergence decision).  The iteration count is integer work and must be equal; the emergent
 spectrum, the F_up / F_down rows, the final T, the whole temperature history and the final
 emit's dtaus are held to 1e-10 outright — no one-ulp floor is folded in (that would need a
@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 
 from tests.parity import assert_grid_parity, row_normwise
-from tests.sharded_oracle import ShardedOracle
+from oracle.sharded import ShardedOracle
 
 pytestmark = pytest.mark.gpu
 
