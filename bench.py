@@ -247,14 +247,17 @@ def binning_leg(a, device, cpu=True):
         for mode, groupies in (("groupies", True), ("exact", False)):
             x.bin(w["wl_bins"], w["lam"], w["T0"], w["p"], groupies=groupies, device=device,
                   out=False)                                   # warm-up (plan + scratch)
-            x.timing(1, device)
+            per = []
             for _ in range(a.binning_reps):
+                x.timing(1, device)
                 x.bin(w["wl_bins"], w["lam"], w["T0"], w["p"], groupies=groupies,
                       device=device, out=False)
-            ms, n = x.timing(0, device)
+                per.append(x.timing(0, device)[0])
+            ms, n = sum(per), len(per)
             acc = binning_bytes(w, groupies)
             t = ms / n * 1e-3
             out[mode] = {"avg_launch_ms": ms / n, "launches": n,
+                         "launch_ms": [round(v, 4) for v in per],
                          "table_values_per_s": acc["dest_rows"] * acc["n_bins"] / t,
                          "source_points_per_s": acc["source_rows"] * acc["points"] / t,
                          "roofline": {"bound": "hbm", "achieved": acc["bytes"] / t / 1e9,

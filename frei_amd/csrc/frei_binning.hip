@@ -11,11 +11,12 @@
 //   groupies (default of binned_opacity): one lane per (source row, bin) walks its bin's
 //     points in order with the reference's float32 accumulator and fans the result out
 //     to every destination (p, T) row that selected this source row (no intermediate);
-//   exact (Grid.load_opacities default): pass 1 integrates each non-empty bin for a
-//     batch of source rows per lane (the dx stream is read once per batch), pass 2
-//     interpolates linearly onto the grid wavelengths and writes every destination row.
+//   exact (Grid.load_opacities default): a block of 256 grid wavelengths integrates the
+//     non-empty bins its interpolation brackets span into LDS, a source-row batch at a time,
+//     then each lane interpolates linearly and fans its value out the same way (no
+//     intermediate array).
 // Both are HBM-bound streams: float32 reads of the selected source rows + float64 writes
-// of the destination table.
+// of the destination table, the writes streaming (non-temporal).
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -42,12 +43,18 @@ struct frei_xsec {
   bool timing = false;
   double t_ms = 0;
   int t_n = 0;
+  // the per-call plan arrays, kept between calls (slot k: device buffer and its capacity in
+  // bytes): no hipMalloc / hipFree per binning call
+  std::vector<std::pair<void*, size_t>> plan;
+  // pinned host staging of the plan uploads (DMA copies; pageable hipMemcpyAsync stalled the
+  // next kernel launch by milliseconds)
+  char* pinned = nullptr;
+  size_t pinned_cap = 0, pinned_used = 0;
 };
 
 namespace {
 
-constexpr int kRB = 4;        // source rows per lane in the exact-mode integration pass
-constexpr int kExpandRows = 8;   // source rows per lane in the exact-mode expand pass
+constexpr int kExactRows = 8;     // source rows per block in the exact mode
 constexpr int kGroupiesRows = 8;  // source rows per lane in the groupies pass
 
 #define HIP_TRY(expr)                                                                   \
@@ -71,6 +78,40 @@ template <typename T>
 void dfree(T*& p) {
   if (p) (void)hipFree((void*)p);
   p = nullptr;
+}
+// Plan array `slot` of x on the device (grown when too small) holding h.
+template <typename T>
+int stage(frei_xsec* x, int slot, T** d, const std::vector<T>& h, hipStream_t st) {
+  if ((int)x->plan.size() <= slot) x->plan.resize(slot + 1, {nullptr, 0});
+  auto& b = x->plan[slot];
+  const size_t need = std::max<size_t>(h.size(), 1) * sizeof(T);
+  if (b.second < need) {
+    if (b.first) (void)hipFree(b.first);
+    b = {nullptr, 0};
+    HIP_TRY(hipMalloc(&b.first, need));
+    b.second = need;
+  }
+  *d = static_cast<T*>(b.first);
+  if (h.empty()) return 0;
+  const size_t n = h.size() * sizeof(T);
+  const size_t at = (x->pinned_used + 255) & ~size_t(255);
+  if (at + n > x->pinned_cap) return set_error("binning: plan staging buffer too small");
+  std::memcpy(x->pinned + at, h.data(), n);
+  x->pinned_used = at + n;
+  HIP_TRY(hipMemcpyAsync(*d, x->pinned + at, n, hipMemcpyHostToDevice, st));
+  return 0;
+}
+// Room for `bytes` of plan uploads in x's pinned staging buffer (grown between calls only: the
+// previous call's copies completed with its stream synchronisation).
+int stage_reserve(frei_xsec* x, size_t bytes) {
+  x->pinned_used = 0;
+  if (bytes <= x->pinned_cap) return 0;
+  if (x->pinned) (void)hipHostFree(x->pinned);
+  x->pinned = nullptr;
+  x->pinned_cap = 0;
+  HIP_TRY(hipHostMalloc((void**)&x->pinned, bytes, hipHostMallocDefault));
+  x->pinned_cap = bytes;
+  return 0;
 }
 template <typename T>
 int upload(T** d, const std::vector<T>& h, hipStream_t st) {
@@ -118,88 +159,97 @@ __global__ __launch_bounds__(256) void bin_groupies_kernel(
       }
     }
     const double v = ((double)acc * wk) * 1e-3;
-    for (int f = fan_off[u]; f < fan_off[u + 1]; ++f) out[fan_dst[f] + k] = v;
+    for (int f = fan_off[u]; f < fan_off[u + 1]; ++f)
+      __builtin_nontemporal_store(v, out + fan_dst[f] + k);   // streaming: written once
   }
 }
 
-// exact, pass 1: xarray integrate (duck_array_ops.trapz) of one non-empty bin for kRB
-// source rows: sum_i (dx_i * 0.5) * f64(f32(y_{i+1} + y_i)) in point order, / (wl_max -
-// wl_min) (opacity.py:40-42; a single-point bin gives 0 / 0 = NaN like the reference).
-// Points are taken four at a time with all loads issued before the ordered adds.
-__global__ __launch_bounds__(256) void bin_exact_integrate_kernel(
-    const float* __restrict__ x, const int64_t* __restrict__ row_off, int U,
+// exact: one block per 256 output wavelengths and a range of source rows [u0, u1) (grid y).
+// Per kExactBatch rows its lanes integrate the non-empty bins [glo, glo + ng) the block's
+// interpolation brackets span into LDS ([kExactBatch][gcap], gcap the largest ng of the
+// launch): xarray integrate (duck_array_ops.trapz), sum_i (dx_i * 0.5) * f64(f32(y_{i+1} + y_i))
+// in point order, / (wl_max - wl_min) (opacity.py:40-42; a single-point bin gives 0 / 0 = NaN
+// like the reference), four points' loads of four rows issued before their ordered adds.  One
+// barrier, then every lane
+// interpolates its wavelength, scipy interp1d(kind='linear', fill_value='extrapolate'):
+// slope = (y_hi - y_lo) / (x_hi - x_lo), y = slope * (x - x_lo) + y_lo, and stores it to every
+// destination row that selected the source row (the groupies fan-out), streaming.  HBM traffic:
+// the selected source rows once (float32; a block boundary's bin is read by both blocks) and the
+// destination table once (float64); no intermediate array.
+constexpr int kExactBatch = 4;      // source rows integrated together (loads in flight)
+__global__ __launch_bounds__(256) void bin_exact_kernel(
+    const float* __restrict__ x, const int64_t* __restrict__ row_off, int U, int rows_per,
     const int64_t* __restrict__ gstart, const int64_t* __restrict__ gend,
-    const double* __restrict__ hdx, const double* __restrict__ Dx, int64_t G,
-    double* __restrict__ res) {
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
-  const int u0 = blockIdx.y * kRB;
-  const int nr = min(kRB, U - u0);
-  const int64_t s = gstart[g], e = gend[g];
-  const float* rows[kRB];
-  double acc[kRB];
-  float prev[kRB];
-#pragma unroll
-  for (int r = 0; r < kRB; ++r) {
-    rows[r] = x + row_off[u0 + (r < nr ? r : 0)];
-    acc[r] = 0.0;
-    prev[r] = rows[r][s];
-  }
-  int64_t i = s;
-  for (; i + 4 < e; i += 4) {
-    double h[4];
-    float b[kRB][4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) h[q] = hdx[i + q];
-#pragma unroll
-    for (int r = 0; r < kRB; ++r)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) b[r][q] = rows[r][i + 1 + q];
-#pragma unroll
-    for (int r = 0; r < kRB; ++r) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc[r] = acc[r] + h[q] * (double)(b[r][q] + prev[r]);
-        prev[r] = b[r][q];
-      }
-    }
-  }
-  for (; i + 1 < e; ++i) {
-    const double h = hdx[i];
-#pragma unroll
-    for (int r = 0; r < kRB; ++r) {
-      const float b = rows[r][i + 1];
-      acc[r] = acc[r] + h * (double)(b + prev[r]);
-      prev[r] = b;
-    }
-  }
-  const double d = Dx[g];
-#pragma unroll
-  for (int r = 0; r < kRB; ++r)
-    if (r < nr) res[(int64_t)(u0 + r) * G + g] = acc[r] / d;
-}
-
-// exact, pass 2: scipy interp1d(kind='linear', fill_value='extrapolate') onto the grid
-// wavelengths, slope = (y_hi - y_lo) / (x_hi - x_lo), y = slope * (x - x_lo) + y_lo.
-// One lane per wavelength and source row (rows [u0, u1)): the bracket is read once per
-// lane, each source value pair once, and the result is stored to every destination row
-// that selected this source row (the groupies fan-out).
-__global__ __launch_bounds__(256) void bin_exact_expand_kernel(
-    const double* __restrict__ res, int64_t G, int U, int rows_per,
+    const double* __restrict__ hdx, const double* __restrict__ Dx,
+    const int32_t* __restrict__ blk_glo, const int32_t* __restrict__ blk_ng, int gcap,
     const int32_t* __restrict__ fan_off, const int64_t* __restrict__ fan_dst,
     const int32_t* __restrict__ lo, const double* __restrict__ xlo,
     const double* __restrict__ xhi, const double* __restrict__ lam, int64_t n,
     double* __restrict__ out) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const int32_t l = lo[j];
-  const double dxj = xhi[j] - xlo[j], t = lam[j] - xlo[j];
+  constexpr int R = kExactBatch;
+  extern __shared__ double integ[];   // [R][gcap]
+  const int tid = threadIdx.x;
+  const int64_t j = (int64_t)blockIdx.x * 256 + tid;
+  const bool act = j < n;
+  const int glo = blk_glo[blockIdx.x], ng = blk_ng[blockIdx.x];
+  const int32_t l = act ? lo[j] - glo : 0;
+  const double dxj = act ? xhi[j] - xlo[j] : 1.0, tj = act ? lam[j] - xlo[j] : 0.0;
   const int u0 = blockIdx.y * rows_per, u1 = min(U, u0 + rows_per);
-  for (int u = u0; u < u1; ++u) {
-    const double* __restrict__ y = res + (int64_t)u * G;
-    const double ylo = y[l], yhi = y[l + 1];
-    const double v = ((yhi - ylo) / dxj) * t + ylo;
-    for (int f = fan_off[u]; f < fan_off[u + 1]; ++f) out[fan_dst[f] + j] = v;
+  for (int ub = u0; ub < u1; ub += R) {
+    const int nr = min(R, u1 - ub);
+    const float* rows[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) rows[r] = x + row_off[ub + (r < nr ? r : 0)];
+    for (int t = tid; t < ng; t += 256) {   // this lane's bins
+      const int64_t s = gstart[glo + t], e = gend[glo + t];
+      double acc[R];
+      float prev[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        acc[r] = 0.0;
+        prev[r] = rows[r][s];
+      }
+      int64_t i = s;
+      for (; i + 4 < e; i += 4) {
+        double h[4];
+        float b[R][4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) h[c] = hdx[i + c];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) b[r][c] = rows[r][i + 1 + c];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            acc[r] = acc[r] + h[c] * (double)(b[r][c] + prev[r]);
+            prev[r] = b[r][c];
+          }
+      }
+      for (; i + 1 < e; ++i) {
+        const double h = hdx[i];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const float b = rows[r][i + 1];
+          acc[r] = acc[r] + h * (double)(b + prev[r]);
+          prev[r] = b;
+        }
+      }
+      const double D = Dx[glo + t];
+#pragma unroll
+      for (int r = 0; r < R; ++r) integ[r * gcap + t] = acc[r] / D;
+    }
+    __syncthreads();
+    if (act) {
+      for (int r = 0; r < nr; ++r) {
+        const double ylo = integ[r * gcap + l], yhi = integ[r * gcap + l + 1];
+        const double v = ((yhi - ylo) / dxj) * tj + ylo;
+        for (int f = fan_off[ub + r]; f < fan_off[ub + r + 1]; ++f)
+          __builtin_nontemporal_store(v, out + fan_dst[f] + j);
+      }
+    }
+    __syncthreads();   // the next rows' integrals overwrite these
   }
 }
 
@@ -321,14 +371,15 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
     for (size_t d = 0; d < dst_src.size(); ++d) fan_dst[fill[dst_src[d]]++] = dest.off[d];
   }
 
-  std::vector<void*> tmp;
-  auto cleanup = [&]() {
-    (void)hipStreamSynchronize(st);
-    for (void* q : tmp) (void)hipFree(q);
-  };
+  // (the host vectors outlive every copy: the stream is synchronised before returning)
+  auto cleanup = [&]() { (void)hipStreamSynchronize(st); };
+  // every plan array of either mode (groups <= bins), with the 256-byte alignment of each
+  const size_t plan_bytes = 4096 + 16 * ((size_t)U + 1) + 8 * fan_dst.size() +
+                            24 * ((size_t)n_bins + 1) + 32 * (size_t)n_out +
+                            8 * ((size_t)n_out / 256 + 1);
+  if (int rc = stage_reserve(x, plan_bytes)) return rc;
   int64_t* d_row = nullptr;
-  if (int rc = upload(&d_row, row_off, st)) return cleanup(), rc;
-  tmp.push_back(d_row);
+  if (int rc = stage(x, 0, &d_row, row_off, st)) return cleanup(), rc;
   hipEvent_t ev[2] = {nullptr, nullptr};
   if (x->timing)
     for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
@@ -342,15 +393,17 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
     int64_t *d_s = nullptr, *d_e = nullptr, *d_fd = nullptr;
     double* d_w = nullptr;
     int32_t* d_fo = nullptr;
-    if ((rc = upload(&d_s, s, st)) || (tmp.push_back(d_s), rc = upload(&d_e, e, st)) ||
-        (tmp.push_back(d_e), rc = upload(&d_w, w, st)) ||
-        (tmp.push_back(d_w), rc = upload(&d_fo, fan_off, st)) ||
-        (tmp.push_back(d_fo), rc = upload(&d_fd, fan_dst, st)))
+    if ((rc = stage(x, 1, &d_s, s, st)) || (rc = stage(x, 2, &d_e, e, st)) ||
+        (rc = stage(x, 3, &d_w, w, st)) || (rc = stage(x, 4, &d_fo, fan_off, st)) ||
+        (rc = stage(x, 5, &d_fd, fan_dst, st)))
       return cleanup(), rc;
-    tmp.push_back(d_fd);
     const int rows_per = std::min(U, kGroupiesRows);
     dim3 grid((unsigned)((n_out + 255) / 256), (unsigned)((U + rows_per - 1) / rows_per));
-    if (x->timing) HIP_TRY(hipEventRecord(ev[0], st));
+    // timed: the plan uploads (pageable copies) complete first, so the events hold the kernel
+    if (x->timing) {
+      HIP_TRY(hipStreamSynchronize(st));
+      HIP_TRY(hipEventRecord(ev[0], st));
+    }
     bin_groupies_kernel<<<grid, 256, 0, st>>>(x->d_x, d_row, U, rows_per, d_s, d_e, d_w, n_out,
                                               d_fo, d_fd, d_out);
   } else {
@@ -375,7 +428,6 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
     }
     const int64_t g0 = *std::min_element(hi.begin(), hi.end()) - 1;
     const int64_t g1 = *std::max_element(hi.begin(), hi.end()) + 1;  // groups [g0, g1)
-    const int64_t G = g1 - g0;
     std::vector<int64_t> s(gs.begin() + g0, gs.begin() + g1), e(ge.begin() + g0, ge.begin() + g1);
     std::vector<double> dx(Dx.begin() + g0, Dx.begin() + g1);
     std::vector<int32_t> lo(n_out);
@@ -385,34 +437,48 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
       xlo[j] = xc[hi[j] - 1];
       xhi[j] = xc[hi[j]];
     }
+    // per block of 256 output wavelengths: the bins its brackets span (lo is non-decreasing in
+    // j, lam being ascending) — about 257 when the wavelengths are the bin centres
+    const int64_t nblk = (n_out + 255) / 256;
+    std::vector<int32_t> bglo(nblk), bng(nblk);
+    int gcap = 1;
+    for (int64_t q = 0; q < nblk; ++q) {
+      const int64_t ja = q * 256, jb = std::min(n_out, ja + 256) - 1;
+      bglo[q] = lo[ja];
+      bng[q] = lo[jb] + 2 - lo[ja];
+      gcap = std::max(gcap, (int)bng[q]);
+    }
+    const size_t lds = (size_t)kExactBatch * gcap * sizeof(double);
+    if (lds > 160 * 1024)
+      return cleanup(), set_error("binning: a block of 256 wavelengths spans more than 5120 bins");
+    if (lds > 64 * 1024)
+      HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&bin_exact_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (!x->d_hdx) {
       std::vector<double> h(std::max<int64_t>(x->nhi - 1, 1));
       for (int64_t i = 0; i + 1 < x->nhi; ++i) h[i] = (wl[i + 1] - wl[i]) * 0.5;
       if ((rc = upload(&x->d_hdx, h, st))) return cleanup(), rc;
     }
     int64_t *d_s = nullptr, *d_e = nullptr, *d_do = nullptr;
-    double *d_D = nullptr, *d_res = nullptr, *d_xlo = nullptr, *d_xhi = nullptr,
-           *d_lam = nullptr;
-    int32_t *d_lo = nullptr, *d_fo = nullptr;
-    if ((rc = upload(&d_s, s, st)) || (tmp.push_back(d_s), rc = upload(&d_e, e, st)) ||
-        (tmp.push_back(d_e), rc = upload(&d_D, dx, st)) ||
-        (tmp.push_back(d_D), rc = dalloc(&d_res, (size_t)U * G)) ||
-        (tmp.push_back(d_res), rc = upload(&d_lo, lo, st)) ||
-        (tmp.push_back(d_lo), rc = upload(&d_xlo, xlo, st)) ||
-        (tmp.push_back(d_xlo), rc = upload(&d_xhi, xhi, st)) ||
-        (tmp.push_back(d_xhi), rc = upload(&d_lam, lamv, st)) ||
-        (tmp.push_back(d_lam), rc = upload(&d_fo, fan_off, st)) ||
-        (tmp.push_back(d_fo), rc = upload(&d_do, fan_dst, st)))
+    double *d_D = nullptr, *d_xlo = nullptr, *d_xhi = nullptr, *d_lam = nullptr;
+    int32_t *d_lo = nullptr, *d_fo = nullptr, *d_bglo = nullptr, *d_bng = nullptr;
+    if ((rc = stage(x, 1, &d_s, s, st)) || (rc = stage(x, 2, &d_e, e, st)) ||
+        (rc = stage(x, 3, &d_D, dx, st)) || (rc = stage(x, 4, &d_fo, fan_off, st)) ||
+        (rc = stage(x, 5, &d_do, fan_dst, st)) || (rc = stage(x, 6, &d_lo, lo, st)) ||
+        (rc = stage(x, 7, &d_xlo, xlo, st)) || (rc = stage(x, 8, &d_xhi, xhi, st)) ||
+        (rc = stage(x, 9, &d_lam, lamv, st)) || (rc = stage(x, 10, &d_bglo, bglo, st)) ||
+        (rc = stage(x, 11, &d_bng, bng, st)))
       return cleanup(), rc;
-    tmp.push_back(d_do);
-    dim3 g1d((unsigned)((G + 255) / 256), (unsigned)((U + kRB - 1) / kRB));
-    if (x->timing) HIP_TRY(hipEventRecord(ev[0], st));
-    bin_exact_integrate_kernel<<<g1d, 256, 0, st>>>(x->d_x, d_row, U, d_s, d_e, x->d_hdx, d_D,
-                                                    G, d_res);
-    const int uper = std::min(U, kExpandRows);
-    dim3 g2d((unsigned)((n_out + 255) / 256), (unsigned)((U + uper - 1) / uper));
-    bin_exact_expand_kernel<<<g2d, 256, 0, st>>>(d_res, G, U, uper, d_fo, d_do, d_lo, d_xlo,
-                                                 d_xhi, d_lam, n_out, d_out);
+    // timed: the plan uploads (pageable copies) complete first, so the events hold the kernel
+    if (x->timing) {
+      HIP_TRY(hipStreamSynchronize(st));
+      HIP_TRY(hipEventRecord(ev[0], st));
+    }
+    const int rows_per = std::min(U, kExactRows);
+    dim3 grid((unsigned)nblk, (unsigned)((U + rows_per - 1) / rows_per));
+    bin_exact_kernel<<<grid, 256, lds, st>>>(x->d_x, d_row, U, rows_per, d_s, d_e, x->d_hdx,
+                                             d_D, d_bglo, d_bng, gcap, d_fo, d_do, d_lo, d_xlo, d_xhi, d_lam,
+                                           n_out, d_out);
   }
   if (hipGetLastError() != hipSuccess) return cleanup(), set_error("binning kernel launch failed");
   if (x->timing) {
@@ -524,6 +590,9 @@ int frei_xsec_destroy(frei_xsec* x) {
   dfree(x->d_x);
   dfree(x->d_hdx);
   dfree(x->d_scratch);
+  for (auto& b : x->plan)
+    if (b.first) (void)hipFree(b.first);
+  if (x->pinned) (void)hipHostFree(x->pinned);
   if (x->stream) (void)hipStreamDestroy(x->stream);
   delete x;
   return 0;

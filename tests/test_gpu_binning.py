@@ -149,3 +149,30 @@ def test_sharded_binning_matches_whole_grid(fa, golden):
                 assert np.array_equal(k[ok], kw[ok]), (groupies, lo, hi)
     finally:
         x.release()
+
+
+@pytest.mark.parametrize("n_pts,n_bins", [(300_001, 3000), (100_001, 60_000)])
+def test_exact_binning_wide_and_sparse_groups_vs_oracle(fa, n_pts, n_bins):
+    """The exact mode's lanes integrate the two bins of their interpolation bracket themselves:
+    at 3000 bins over 300k points each bin holds ~100 points (the four-point load batches and
+    their tails); at 60k bins over 100k points a fifth of the bins are empty and over a third hold
+    one point (brackets between non-adjacent bins, NaN from single-point bins), with one source row fanned out to
+    several table rows.  Bit for bit the oracle (same summation order)."""
+    rng = np.random.default_rng(12)
+    nu = np.linspace(1000.0, 20000.0, n_pts)
+    wl = (1e4 / nu)[1:][::-1]
+    T_src, p_src = np.array([800.0, 1600.0, 2400.0]), np.array([1e-3, 1.0])
+    xsec = (10 ** rng.uniform(-4, 2, (3, 2, wl.size))).astype(np.float32)
+    lam, wl_bins, _ = O.wavelength_grid(0.5, 10, n_bins)
+    T_t = np.array([700.0, 900.0, 1500.0, 2600.0, 3000.0])
+    p_t = np.array([1e-4, 1e-2, 0.8, 5.0])
+    x = fa.CrossSection(xsec, T_src, p_src, wl)
+    try:
+        out = x.bin(wl_bins, lam, T_t, p_t, groupies=False)
+    finally:
+        x.release()
+    ref = O.binned_opacity(xsec, T_src, p_src, wl, T_t, p_t, wl_bins, lam, False)
+    assert np.array_equal(np.isnan(out), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert np.array_equal(out[ok], ref[ok])
+    assert ok.mean() > 0.2
