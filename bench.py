@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--rad-eq-max", type=int, default=200,
                     help="max T-P iterations for the iterations-to-radiative-equilibrium run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-lam", type=int, default=50_000)
+    ap.add_argument("--cpu-lam", type=int, default=500_000)
     ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
                     help="worker processes of the all-cores CPU leg (1 = skip it; the GPU box "
                          "grants a 16-CPU share)")

@@ -1,6 +1,10 @@
 """Summarise rocprofv3 PMC runs into per-launch HBM traffic of the sweep kernel.
 
     python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [--n-lam N --n-layers L --species S]
+                                [--kernel NAME --contracted 0|1]
+
+--kernel (default sweep_pair_kernel, the headline sweep) selects the dispatches by name: a bench
+run also holds the per-species leg's sweep (sweep_fast_kernel, --contracted=0).
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts exactly half
 of the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md, HBM section), so
@@ -13,10 +17,10 @@ import json
 import sys
 
 
-def per_kernel(path, counter):
+def per_kernel(path, counter, name):
     vals = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter or "sweep" not in r["Kernel_Name"]:
+        if r["Counter_Name"] != counter or name not in r["Kernel_Name"]:
             continue
         vals.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]) * 1024.0)
     return {k: statistics.median(v) for k, v in vals.items()}
@@ -29,8 +33,9 @@ def main():
     nL = int(opts.get("n-layers", 60))
     S = int(opts.get("species", 8))
     contracted = opts.get("contracted", "1") == "1"   # K3: the sweep reads one table
-    fetch = per_kernel(f"{fdir}/run_counter_collection.csv", "FETCH_SIZE")
-    write = per_kernel(f"{wdir}/run_counter_collection.csv", "WRITE_SIZE")
+    name = opts.get("kernel", "sweep_pair_kernel")
+    fetch = per_kernel(f"{fdir}/run_counter_collection.csv", "FETCH_SIZE", name)
+    write = per_kernel(f"{wdir}/run_counter_collection.csv", "WRITE_SIZE", name)
     kernels = {}
     for k in fetch:
         rd = 2.0 * fetch[k]

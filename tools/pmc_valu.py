@@ -1,13 +1,14 @@
 """VALU utilisation of the sweep kernel from a rocprofv3 SQ counter pass.
 
-    python tools/pmc_valu.py SQ_DIR OUT.json [--n-lam N --n-layers L]
+    python tools/pmc_valu.py SQ_DIR OUT.json [--n-lam N --n-layers L --kernel NAME]
 
 Counters (one pass): SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, SQ_WAVES, SQ_WAVE_CYCLES,
 SQ_BUSY_CYCLES, GRBM_GUI_ACTIVE.  SQ_ACTIVE_INST_VALU counts quad-cycles summed over waves;
 GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md), so
   valu_busy = 4 * SQ_ACTIVE_INST_VALU / (1024 SIMDs * GRBM_GUI_ACTIVE / 8)
 and VALU wave-instructions per flux update = SQ_INSTS_VALU * 64 / updates per launch.
-Median over the sweep-kernel dispatches.
+Median over the dispatches of the kernel named by --kernel (default sweep_pair_kernel, the
+headline sweep; sweep_fast_kernel for the per-species leg).
 """
 import csv
 import json
@@ -20,9 +21,10 @@ def main():
     opts = dict(a.lstrip("-").split("=") for a in sys.argv[3:])
     n_lam = int(opts.get("n-lam", 500000))
     nL = int(opts.get("n-layers", 60))
+    name = opts.get("kernel", "sweep_pair_kernel")
     per = {}
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-        if "sweep" not in r["Kernel_Name"]:
+        if name not in r["Kernel_Name"]:
             continue
         key = (r["Dispatch_Id"], r["Kernel_Name"])
         per.setdefault(key, {})[r["Counter_Name"]] = float(r["Counter_Value"])
