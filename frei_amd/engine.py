@@ -335,12 +335,14 @@ class Engine:
         T = self.get_temperatures()
         hists = []
         it = 0
+        dT = np.empty(nL)
         for it in range(1, int(n_timesteps) + 1):
             self._provider_step(T)
-            self.sweep(EMIT, alpha=alpha, want_dtaus=False)
+            # (the loop reads back only what it uses: no bolometric sums, no emit dT)
+            N.check(N.lib().frei_sweep(self._ctx, EMIT, float(alpha), None, None, None))
             T1 = self.get_temperatures()
             self._provider_step(T1)
-            dT, _, _ = self.sweep(ABSORB, alpha=alpha, want_dtaus=False)
+            N.check(N.lib().frei_sweep(self._ctx, ABSORB, float(alpha), N.dptr(dT), None, None))
             T = self.get_temperatures()
             hists.append(np.stack([T1, T], axis=1))
             th = np.hstack(hists)
