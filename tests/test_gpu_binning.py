@@ -176,3 +176,54 @@ def test_exact_binning_wide_and_sparse_groups_vs_oracle(fa, n_pts, n_bins):
     ok = ~np.isnan(ref)
     assert np.array_equal(out[ok], ref[ok])
     assert ok.mean() > 0.2
+
+
+def test_plan_buffers_reused_across_grids(fa):
+    """The plan arrays stay on the device between calls (grown when a call needs more): binning
+    onto a fine grid, a coarse one, the fine one again and then the coarse one in the other mode
+    with one CrossSection gives each call's result bit for bit what a fresh CrossSection gives."""
+    rng = np.random.default_rng(13)
+    nu = np.linspace(1000.0, 20000.0, 200_001)
+    wl = (1e4 / nu)[1:][::-1]
+    T_src, p_src = np.array([800.0, 1600.0, 2400.0]), np.array([1e-3, 1.0])
+    xsec = (10 ** rng.uniform(-4, 2, (3, 2, wl.size))).astype(np.float32)
+    fine = O.wavelength_grid(0.5, 10, 40_000)
+    coarse = O.wavelength_grid(0.7, 8, 2_500)
+    T_t, p_t = np.array([700.0, 1500.0, 2600.0]), np.array([1e-4, 0.8, 5.0])
+    calls = [(fine, False), (coarse, False), (fine, False), (coarse, True), (fine, True)]
+    x = fa.CrossSection(xsec, T_src, p_src, wl)
+    try:
+        reused = [x.bin(g[1], g[0], T_t, p_t, groupies=gr) for g, gr in calls]
+    finally:
+        x.release()
+    for (g, gr), out in zip(calls, reused):
+        y = fa.CrossSection(xsec, T_src, p_src, wl)
+        try:
+            fresh = y.bin(g[1], g[0], T_t, p_t, groupies=gr)
+        finally:
+            y.release()
+        assert np.array_equal(out, fresh, equal_nan=True), (g[0].size, gr)
+
+
+def test_exact_binning_wavelengths_far_from_bin_centres(fa):
+    """interp1d takes any ascending wavelengths: here the first 1000 skip ~12 bins each, so a
+    block of 256 output wavelengths spans ~3000 bins (96 KiB of integrals in LDS, above the
+    64 KiB a launch gets without opting in), and the other 19000 crowd the last 40 % of the bins.
+    Bit for bit the oracle."""
+    nu = np.linspace(1000.0, 20000.0, 300_001)
+    wl = (1e4 / nu)[1:][::-1]
+    lam0, wl_bins, _ = O.wavelength_grid(0.5, 10, 20_000)
+    lam = np.concatenate([lam0[np.linspace(0, 11999, 1000).astype(int)],
+                          np.linspace(lam0[12000], lam0[-1], 19000)])
+    rng = np.random.default_rng(14)
+    T_src, p_src = np.array([800.0, 1600.0]), np.array([1e-3, 1.0])
+    xsec = (10 ** rng.uniform(-4, 2, (2, 2, wl.size))).astype(np.float32)
+    T_t, p_t = np.array([900.0, 1500.0]), np.array([1e-2, 0.8])
+    x = fa.CrossSection(xsec, T_src, p_src, wl)
+    try:
+        out = x.bin(wl_bins, lam, T_t, p_t, groupies=False)
+    finally:
+        x.release()
+    ref = O.binned_opacity(xsec, T_src, p_src, wl, T_t, p_t, wl_bins, lam, False)
+    assert np.isfinite(ref).all()
+    assert np.array_equal(out, ref)
