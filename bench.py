@@ -633,8 +633,8 @@ def main():
                "kind": "port",
                "sample": f"oracle (NumPy restatement of frei's path, single-threaded: 1 of "
                          f"{os.cpu_count()} host CPUs), {nL} layers x {min(a.cpu_lam, n_lam)} "
-                         f"lambda (evenly strided sample of the same grid), {S} species, 1 T-P "
-                         f"iteration + final emit, {dt:.1f} s"}
+                         f"lambda ({'the whole grid' if a.cpu_lam >= n_lam else 'evenly strided sample of the same grid'}), "
+                         f"{S} species, 1 T-P iteration + final emit, {dt:.1f} s"}
         cpu["reference_measured"] = dict(REFERENCE_MEASURED,
                                          port_over_reference=rate / REFERENCE_MEASURED["value"],
                                          note="the port's figure is 8 species (K3 not used: "
