@@ -560,7 +560,10 @@ __device__ __forceinline__ unsigned long long chain_poll(const FastArgs& a, cons
   while (eq ? (v >> 2) != want : v == until_not) {
     __builtin_amdgcn_s_sleep(1);
     v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (wall_clock64() - t0 > a.ch_timeout) {
+    // after one timeout every later wait gives up at once (the run has already failed): a
+    // block's per-layer waits then end within one timeout, not one each
+    if (wall_clock64() - t0 > a.ch_timeout ||
+        __hip_atomic_load(a.ch_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
       __hip_atomic_store(a.ch_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
