@@ -56,6 +56,7 @@ namespace {
 
 constexpr int kExactRows = 8;     // source rows per block in the exact mode
 constexpr int kGroupiesRows = 8;  // source rows per lane in the groupies pass
+constexpr int kGroupiesBatch = 4; // of which summed together (loads in flight)
 
 #define HIP_TRY(expr)                                                                   \
   do {                                                                                  \
@@ -132,35 +133,55 @@ __global__ __launch_bounds__(256) void bin_groupies_kernel(
     const int64_t* __restrict__ start, const int64_t* __restrict__ end,
     const double* __restrict__ width, int64_t nb, const int32_t* __restrict__ fan_off,
     const int64_t* __restrict__ fan_dst, double* __restrict__ out) {
+  constexpr int R = kGroupiesBatch;
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nb) return;
   const int64_t s = start[k], e = end[k];
   const double wk = width[k];
   const int u0 = blockIdx.y * rows_per, u1 = min(U, u0 + rows_per);
-  for (int u = u0; u < u1; ++u) {
-    const float* __restrict__ row = x + row_off[u];
-    float acc = 0.0f;
+  for (int ub = u0; ub < u1; ub += R) {   // R source rows at a time: their loads in flight together
+    const int nr = min(R, u1 - ub);
+    const float* rows[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) rows[r] = x + row_off[ub + (r < nr ? r : 0)];
+    float acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.0f;
     if (e - s >= 2) {
-      float a = row[s];
+      float a[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) a[r] = rows[r][s];
       int64_t i = s + 1;
-      // four loads in flight per lane; the accumulation order stays sequential
+      // four points of every row loaded before the ordered adds (each row's sequence unchanged)
       for (; i + 4 <= e; i += 4) {
-        const float b0 = row[i], b1 = row[i + 1], b2 = row[i + 2], b3 = row[i + 3];
-        acc = (float)((double)acc + (double)(a + b0) / 2.0);
-        acc = (float)((double)acc + (double)(b0 + b1) / 2.0);
-        acc = (float)((double)acc + (double)(b1 + b2) / 2.0);
-        acc = (float)((double)acc + (double)(b2 + b3) / 2.0);
-        a = b3;
+        float b[R][4];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) b[r][c] = rows[r][i + c];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          acc[r] = (float)((double)acc[r] + (double)(a[r] + b[r][0]) / 2.0);
+          acc[r] = (float)((double)acc[r] + (double)(b[r][0] + b[r][1]) / 2.0);
+          acc[r] = (float)((double)acc[r] + (double)(b[r][1] + b[r][2]) / 2.0);
+          acc[r] = (float)((double)acc[r] + (double)(b[r][2] + b[r][3]) / 2.0);
+          a[r] = b[r][3];
+        }
       }
       for (; i < e; ++i) {
-        const float b = row[i];
-        acc = (float)((double)acc + (double)(a + b) / 2.0);
-        a = b;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const float b = rows[r][i];
+          acc[r] = (float)((double)acc[r] + (double)(a[r] + b) / 2.0);
+          a[r] = b;
+        }
       }
     }
-    const double v = ((double)acc * wk) * 1e-3;
-    for (int f = fan_off[u]; f < fan_off[u + 1]; ++f)
-      __builtin_nontemporal_store(v, out + fan_dst[f] + k);   // streaming: written once
+    for (int r = 0; r < nr; ++r) {
+      const double v = ((double)acc[r] * wk) * 1e-3;
+      for (int f = fan_off[ub + r]; f < fan_off[ub + r + 1]; ++f)
+        __builtin_nontemporal_store(v, out + fan_dst[f] + k);   // streaming: written once
+    }
   }
 }
 
