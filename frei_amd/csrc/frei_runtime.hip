@@ -184,6 +184,15 @@ struct frei_ctx {
   int32_t *d_flips = nullptr, *d_prev = nullptr, *d_ndiff = nullptr;
   int* h_flag = nullptr;  // pinned [2]
   int* h_err = nullptr;   // pinned [2]: the chained-poll and P2P error flags (check_comm)
+  // pinned staging of the per-sweep host round trip of a chemistry provider stepping the loop
+  // (frei_get_temperatures, frei_sweep's dT / bolometric sums, frei_set_mmr's upload): one
+  // stream synchronisation per read, none for the upload (pageable copies add their own)
+  double* h_T = nullptr;     // [n_layers * n_atm]
+  double* h_dT = nullptr;    // [n_layers]
+  double* h_bol = nullptr;   // [n_layers * 4]
+  double* h_mmr = nullptr;   // [n_species * n_layers * n_atm]
+  hipEvent_t mmr_ev = nullptr;   // the last upload from h_mmr
+  bool mmr_ev_set = false;
   int64_t chain_checked = 0;   // n_chained at the last check_comm
   hipEvent_t flag_ev[2] = {nullptr, nullptr};
   // comm
@@ -457,7 +466,14 @@ double now_ms() {
 int build_meta(frei_ctx* c) {
   if (!c->meta_dirty) {
     if (c->mmr_dirty) {   // new mixing ratios only: up on the stream, ahead of the next sweep
-      TRY(h2d(c->d_mmr, c->mmr.data(), c->mmr.size(), c->stream));
+      // (through pinned staging, no synchronisation: the previous upload from it has finished
+      // once its event has)
+      if (c->mmr_ev_set) HIP_TRY(hipEventSynchronize(c->mmr_ev));
+      std::memcpy(c->h_mmr, c->mmr.data(), c->mmr.size() * sizeof(double));
+      HIP_TRY(hipMemcpyAsync(c->d_mmr, c->h_mmr, c->mmr.size() * sizeof(double),
+                             hipMemcpyHostToDevice, c->stream));
+      HIP_TRY(hipEventRecord(c->mmr_ev, c->stream));
+      c->mmr_ev_set = true;
       c->mmr_dirty = false;
     }
     return 0;
@@ -1251,6 +1267,12 @@ static int ctx_create(frei_ctx** out, int device, int n_layers, int64_t n_lam, i
     return bail(fail("hipMemsetAsync failed"));
   if (A > 1 && hipHostMalloc((void**)&c->h_conv, 2 * A * sizeof(int)) != hipSuccess)
     return bail(fail("hipHostMalloc failed"));
+  if (hipHostMalloc((void**)&c->h_T, NL * A * sizeof(double)) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_dT, NL * sizeof(double)) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_bol, NL * 4 * sizeof(double)) != hipSuccess ||
+      hipHostMalloc((void**)&c->h_mmr, (size_t)n_species * NL * A * sizeof(double)) != hipSuccess ||
+      hipEventCreateWithFlags(&c->mmr_ev, hipEventDisableTiming) != hipSuccess)
+    return bail(fail("hipHostMalloc failed"));
   *out = c;
   return 0;
 }
@@ -1304,6 +1326,9 @@ int frei_ctx_destroy(frei_ctx* c) {
   if (c->h_flag) (void)hipHostFree(c->h_flag);
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_conv) (void)hipHostFree(c->h_conv);
+  for (double* h : {c->h_T, c->h_dT, c->h_bol, c->h_mmr})
+    if (h) (void)hipHostFree(h);
+  if (c->mmr_ev) (void)hipEventDestroy(c->mmr_ev);
   dfree(c->d_g);
   if (c->h_ag) (void)hipHostFree(c->h_ag);
   for (auto e : c->flag_ev)
@@ -1616,8 +1641,10 @@ int frei_set_temperatures(frei_ctx* c, const double* T) {
 int frei_get_temperatures(frei_ctx* c, double* T) {
   if (!c || !T) return fail("null argument");
   TRY(set_device(c));
+  const size_t n = (size_t)c->nL * c->n_atm;
+  HIP_TRY(hipMemcpyAsync(c->h_T, c->d_T, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  HIP_TRY(hipMemcpy(T, c->d_T, (size_t)c->nL * c->n_atm * sizeof(double), hipMemcpyDeviceToHost));
+  std::memcpy(T, c->h_T, n * sizeof(double));
   return 0;
 }
 
@@ -1642,11 +1669,16 @@ int frei_sweep(frei_ctx* c, int direction, double alpha, double* dT, double* bol
   launch_setup(setup_args(c), direction, c->stream);
   HIP_TRY(hipGetLastError());
   TRY(run_sweep(c, o));
+  // the small results through pinned staging, ordered on the stream: one synchronisation
+  if (dT) HIP_TRY(hipMemcpyAsync(c->h_dT, c->d_dT, c->nL * sizeof(double), hipMemcpyDeviceToHost,
+                                 c->stream));
+  if (bol) HIP_TRY(hipMemcpyAsync(c->h_bol, c->d_bol, c->nL * 4 * sizeof(double),
+                                  hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   TRY(check_comm(c));
-  if (dT) HIP_TRY(hipMemcpy(dT, c->d_dT, c->nL * sizeof(double), hipMemcpyDeviceToHost));
+  if (dT) std::memcpy(dT, c->h_dT, c->nL * sizeof(double));
   if (bol) {
-    HIP_TRY(hipMemcpy(bol, c->d_bol, c->nL * 4 * sizeof(double), hipMemcpyDeviceToHost));
+    std::memcpy(bol, c->h_bol, c->nL * 4 * sizeof(double));
     // rows of layers a sweep does not visit are undefined on the device: zero them
     const int skip = (direction == FREI_EMIT) ? 0 : c->nL - 1;
     for (int q = 0; q < 4; ++q) bol[skip * 4 + q] = 0.0;
