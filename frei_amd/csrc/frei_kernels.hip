@@ -1309,7 +1309,8 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
     a.ftoa += m * a.bs.ftoa;
     a.conv += m;
   }
-  if (!a.force && *a.conv) return;
+  // the convergence flag: loaded now, tested once the first steps' loads are in flight (below)
+  const bool conv0 = *a.conv && !a.force;   // (unconditional load: issued at once)
   TRACE_DECL;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1354,6 +1355,7 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
   load_stale(0, sb[0]);
   load_stale(1, sb[1]);
   ring_fence();
+  if (conv0) return;   // converged: nothing stored yet
   double* tile = red + (int64_t)(kBlock / 64) * ns * 4;
   for (int k0 = 0; k0 < ns; k0 += 2) {
     progress_priority(k0, ns);
@@ -1568,7 +1570,9 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
     a.ftoa += m * a.bs.ftoa;
     a.conv += m;
   }
-  if (!CH && !a.force && *a.conv) return;
+  // the convergence flag: loaded now, tested once the step records' loads are in flight (below),
+  // not a round trip of its own ahead of them
+  const bool conv0 = !CH && *a.conv && !a.force;
   TRACE_DECL;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1599,11 +1603,13 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
   // which is not in use yet) or copied from the global step table
   FastStepS* lrec = reinterpret_cast<FastStepS*>(red + (int64_t)NC * ns * 4);
   if (a.rec_on) {
+    if (conv0) return;
     if (stage_records(a, DIR, lrec, lds)) return;
   } else {
     const double* g = reinterpret_cast<const double*>(ss);
     double* l = reinterpret_cast<double*>(lrec);
     for (int idx = tid; idx < ns * kStepDoubles; idx += 256 * NC) l[idx] = g[idx];
+    if (conv0) return;   // block-uniform, ahead of the barrier
     __syncthreads();
   }
   TRACE_MARK(1);
@@ -2395,11 +2401,9 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
   // dT's flux-independent part while the partial sums load (lanes 0, 1: layers l, l + 1)
   LayerPre pre{};
   if (tid < 2 && kd >= 0) pre = layer_pre(T1, T2, p1, p2, lnp, a.su.g, a.m_bar, a.alpha);
-  if (!a.force && conv) {    // converged: carry T into the output buffer
-    if (tid == 0 && on) publish_T(a, l, Tl, conv, true);
-    return;
-  }
-  // ---- this rank's sums, reduce_kernel's order (strided per thread, wave butterfly, waves)
+  // ---- this rank's sums, reduce_kernel's order (strided per thread, wave butterfly, waves),
+  // loaded before the convergence test below (one round trip less on the update's critical
+  // path; a converged run's update only discards them)
   if (k0 >= 0 || k1 >= 0) {
     const double* pj[8];
     for (int j = 0; j < 8; ++j) {
@@ -2440,6 +2444,10 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
       acc[j] = butterfly_sum(acc[j], tid & 63);   // = the xor-32 ... 1 shfl butterfly
     if ((tid & 63) == 0)
       for (int j = 0; j < 8; ++j) wsum[tid >> 6][j] = acc[j];
+  }
+  if (!a.force && conv) {    // converged: carry T into the output buffer (no barrier passed)
+    if (tid == 0 && on) publish_T(a, l, Tl, conv, true);
+    return;
   }
   // stage the setup's inputs in LDS (their loads were issued at the start)
   if (tid < ntn) sNodes[tid] = rNode;
