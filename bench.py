@@ -11,9 +11,11 @@ sharded over N ranks (strong scaling) with one exchange of the per-sweep partial
 engine's P2P mailboxes over xGMI by default).
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
-      (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...; the
-      launcher only starts the processes: rendezvous, barriers and timing reductions go over
-      plain sockets, the per-sweep exchange is the engine's own)
+      (N > 1 either under a launcher — python -m torch.distributed.run --nproc-per-node N
+      bench.py --gpus N ... — or on its own: without WORLD_SIZE in the environment the process
+      starts N rank processes of itself (launch_ranks) before anything touches the GPU and prints
+      rank 0's line.  Rendezvous, barriers and timing reductions go over plain sockets, the
+      per-sweep exchange is the engine's own)
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -85,7 +87,52 @@ def parse():
                     help="skip the batched-atmosphere (C5) measurement")
     ap.add_argument("--c5-lam", type=int, default=100_000)
     ap.add_argument("--c5-steps", type=int, default=5)
+    ap.add_argument("--launch-selftest", action="store_true",
+                    help=argparse.SUPPRESS)   # ranks rendezvous and report, no GPU (CPU test)
     return ap.parse_args()
+
+
+def launch_ranks(a):
+    """`--gpus N` without a launcher: start N rank processes of this script (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR / MASTER_PORT set for each; the rendezvous is frei_amd.rendezvous
+    over 127.0.0.1), forward their stderr, and return rank 0's JSON line.  Runs before anything
+    in this process touches the GPU (nothing is imported from frei_amd here), and the ranks are
+    child processes, never an exec of this one.  Any rank failing fails the launch: the others
+    are terminated and the first non-zero exit status is returned."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else
+                                      subprocess.DEVNULL))
+    import threading
+    out = []
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    rc = 0
+    while True:
+        bad = [p.returncode for p in procs if p.poll() is not None and p.returncode != 0]
+        if bad:   # one rank failed: the others would only wait for it at the next barrier
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            break
+        if all(p.poll() is not None for p in procs):
+            break
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    reader.join(timeout=10)
+    text = out[0].decode() if out else ""
+    lines = [x for x in text.splitlines() if x.strip()]
+    return rc, (lines[-1] if lines else None)
 
 
 class Dist:
@@ -452,9 +499,27 @@ def sweep_kernel_time(eng, n_iter):
 def main():
     _reserve_stdout()
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:   # no launcher: start the ranks here
+        rc, line = launch_ranks(a)
+        if line is not None and rc == 0:
+            os.write(_RESULT_FD, (line + "\n").encode())
+        if rc == 0 and line is None:
+            rc = 1
+        sys.exit(rc)
     # a peer that never publishes its sums fails the run after this long instead of 30 s
     os.environ.setdefault("FREI_P2P_TIMEOUT_S", "10")
     d = Dist(a.gpus)
+    if a.launch_selftest:   # the launch path alone (CPU test): rendezvous, barrier, max, line
+        if os.environ.get("FREI_LAUNCH_SELFTEST_FAIL") == str(d.rank):
+            sys.exit(3)
+        d.barrier()
+        t = d.max(float(d.rank))
+        if d.rank == 0:
+            _emit_result({"metric": "launch selftest", "n_gpus": d.world, "value": t,
+                          "pids": [int(x) for x in d.gather(os.getpid())]})
+        else:
+            d.gather(os.getpid())
+        return
     from frei_amd import _native as N
     from frei_amd.engine import partition
     from frei_amd.opacity import SeparableTable

@@ -102,9 +102,11 @@ int stage(frei_xsec* x, int slot, T** d, const std::vector<T>& h, hipStream_t st
   HIP_TRY(hipMemcpyAsync(*d, x->pinned + at, n, hipMemcpyHostToDevice, st));
   return 0;
 }
-// Room for `bytes` of plan uploads in x's pinned staging buffer (grown between calls only: the
-// previous call's copies completed with its stream synchronisation).
+// Room for `bytes` of plan uploads in x's pinned staging buffer.  The stream is synchronised
+// first: no copy out of the buffer may still be in flight when it is reused or freed (every
+// bin_into path already ends synchronised; this keeps the invariant local).
 int stage_reserve(frei_xsec* x, size_t bytes) {
+  HIP_TRY(hipStreamSynchronize(x->stream));
   x->pinned_used = 0;
   if (bytes <= x->pinned_cap) return 0;
   if (x->pinned) (void)hipHostFree(x->pinned);
@@ -198,6 +200,54 @@ __global__ __launch_bounds__(256) void bin_groupies_kernel(
 // the selected source rows once (float32; a block boundary's bin is read by both blocks) and the
 // destination table once (float64); no intermediate array.
 constexpr int kExactBatch = 4;      // source rows integrated together (loads in flight)
+constexpr int kExactCap = 160 * 1024 / (kExactBatch * 8);   // bins of one block's LDS window
+
+// The integrals of bin [s, e) (width D) of nr <= R source rows: trapz in point order (above),
+// four points' loads of every row in flight before their ordered adds.
+template <int R>
+__device__ __forceinline__ void bin_integrals(const float* const (&rows)[R], int64_t s, int64_t e,
+                                              const double* __restrict__ hdx, double D,
+                                              double (&out)[R]) {
+  double acc[R];
+  float prev[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    acc[r] = 0.0;
+    prev[r] = rows[r][s];
+  }
+  int64_t i = s;
+  for (; i + 4 < e; i += 4) {
+    double h[4];
+    float b[R][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) h[c] = hdx[i + c];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) b[r][c] = rows[r][i + 1 + c];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        acc[r] = acc[r] + h[c] * (double)(b[r][c] + prev[r]);
+        prev[r] = b[r][c];
+      }
+  }
+  for (; i + 1 < e; ++i) {
+    const double h = hdx[i];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float b = rows[r][i + 1];
+      acc[r] = acc[r] + h * (double)(b + prev[r]);
+      prev[r] = b;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) out[r] = acc[r] / D;
+}
+
+// A block whose wavelengths' brackets span more than kExactCap bins (sparse wavelengths over a
+// fine bin grid) has ng < 0: each lane integrates its own two bins (no LDS window, no barrier).
 __global__ __launch_bounds__(256) void bin_exact_kernel(
     const float* __restrict__ x, const int64_t* __restrict__ row_off, int U, int rows_per,
     const int64_t* __restrict__ gstart, const int64_t* __restrict__ gend,
@@ -212,7 +262,7 @@ __global__ __launch_bounds__(256) void bin_exact_kernel(
   const int tid = threadIdx.x;
   const int64_t j = (int64_t)blockIdx.x * 256 + tid;
   const bool act = j < n;
-  const int glo = blk_glo[blockIdx.x], ng = blk_ng[blockIdx.x];
+  const int glo = blk_glo[blockIdx.x], ng = blk_ng[blockIdx.x];   // block-uniform
   const int32_t l = act ? lo[j] - glo : 0;
   const double dxj = act ? xhi[j] - xlo[j] : 1.0, tj = act ? lam[j] - xlo[j] : 0.0;
   const int u0 = blockIdx.y * rows_per, u1 = min(U, u0 + rows_per);
@@ -221,45 +271,25 @@ __global__ __launch_bounds__(256) void bin_exact_kernel(
     const float* rows[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) rows[r] = x + row_off[ub + (r < nr ? r : 0)];
-    for (int t = tid; t < ng; t += 256) {   // this lane's bins
-      const int64_t s = gstart[glo + t], e = gend[glo + t];
-      double acc[R];
-      float prev[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        acc[r] = 0.0;
-        prev[r] = rows[r][s];
-      }
-      int64_t i = s;
-      for (; i + 4 < e; i += 4) {
-        double h[4];
-        float b[R][4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) h[c] = hdx[i + c];
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) b[r][c] = rows[r][i + 1 + c];
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            acc[r] = acc[r] + h[c] * (double)(b[r][c] + prev[r]);
-            prev[r] = b[r][c];
-          }
-      }
-      for (; i + 1 < e; ++i) {
-        const double h = hdx[i];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const float b = rows[r][i + 1];
-          acc[r] = acc[r] + h * (double)(b + prev[r]);
-          prev[r] = b;
+    if (ng < 0) {   // per-lane brackets
+      if (act) {
+        const int g = glo + l;
+        double ylo[R], yhi[R];
+        bin_integrals<R>(rows, gstart[g], gend[g], hdx, Dx[g], ylo);
+        bin_integrals<R>(rows, gstart[g + 1], gend[g + 1], hdx, Dx[g + 1], yhi);
+        for (int r = 0; r < nr; ++r) {
+          const double v = ((yhi[r] - ylo[r]) / dxj) * tj + ylo[r];
+          for (int f = fan_off[ub + r]; f < fan_off[ub + r + 1]; ++f)
+            __builtin_nontemporal_store(v, out + fan_dst[f] + j);
         }
       }
-      const double D = Dx[glo + t];
+      continue;
+    }
+    for (int t = tid; t < ng; t += 256) {   // this lane's bins
+      double v[R];
+      bin_integrals<R>(rows, gstart[glo + t], gend[glo + t], hdx, Dx[glo + t], v);
 #pragma unroll
-      for (int r = 0; r < R; ++r) integ[r * gcap + t] = acc[r] / D;
+      for (int r = 0; r < R; ++r) integ[r * gcap + t] = v[r];
     }
     __syncthreads();
     if (act) {
@@ -392,8 +422,15 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
     for (size_t d = 0; d < dst_src.size(); ++d) fan_dst[fill[dst_src[d]]++] = dest.off[d];
   }
 
-  // (the host vectors outlive every copy: the stream is synchronised before returning)
-  auto cleanup = [&]() { (void)hipStreamSynchronize(st); };
+  // (the host vectors outlive every copy: the stream is synchronised before returning, on every
+  // path once a plan copy may be in flight, so the next call's stage_reserve never frees or
+  // overwrites the pinned buffer under a running DMA; the timing events are destroyed there too)
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  auto cleanup = [&]() {
+    (void)hipStreamSynchronize(st);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+  };
   // every plan array of either mode (groups <= bins), with the 256-byte alignment of each
   const size_t plan_bytes = 4096 + 16 * ((size_t)U + 1) + 8 * fan_dst.size() +
                             24 * ((size_t)n_bins + 1) + 32 * (size_t)n_out +
@@ -401,9 +438,9 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
   if (int rc = stage_reserve(x, plan_bytes)) return rc;
   int64_t* d_row = nullptr;
   if (int rc = stage(x, 0, &d_row, row_off, st)) return cleanup(), rc;
-  hipEvent_t ev[2] = {nullptr, nullptr};
   if (x->timing)
-    for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+    for (auto& e : ev)
+      if (hipEventCreate(&e) != hipSuccess) return cleanup(), set_error("hipEventCreate failed");
   int rc = 0;
   if (mode == FREI_BIN_GROUPIES) {
     // bins [lam_lo, lam_lo + n_out) map 1:1 to output wavelengths
@@ -421,10 +458,9 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
     const int rows_per = std::min(U, kGroupiesRows);
     dim3 grid((unsigned)((n_out + 255) / 256), (unsigned)((U + rows_per - 1) / rows_per));
     // timed: the plan uploads (pageable copies) complete first, so the events hold the kernel
-    if (x->timing) {
-      HIP_TRY(hipStreamSynchronize(st));
-      HIP_TRY(hipEventRecord(ev[0], st));
-    }
+    if (x->timing && (hipStreamSynchronize(st) != hipSuccess ||
+                      hipEventRecord(ev[0], st) != hipSuccess))
+      return cleanup(), set_error("binning: timing event failed");
     bin_groupies_kernel<<<grid, 256, 0, st>>>(x->d_x, d_row, U, rows_per, d_s, d_e, d_w, n_out,
                                               d_fo, d_fd, d_out);
   } else {
@@ -458,23 +494,31 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
       xlo[j] = xc[hi[j] - 1];
       xhi[j] = xc[hi[j]];
     }
-    // per block of 256 output wavelengths: the bins its brackets span (lo is non-decreasing in
-    // j, lam being ascending) — about 257 when the wavelengths are the bin centres
+    // per block of 256 output wavelengths: the bins its brackets span, from the smallest to
+    // the largest lo of its lanes (any order of lam: scipy's interp1d takes unsorted x_new) —
+    // about 257 when the wavelengths are the bin centres; a block spanning more than kExactCap
+    // bins interpolates lane by lane (bng < 0)
     const int64_t nblk = (n_out + 255) / 256;
     std::vector<int32_t> bglo(nblk), bng(nblk);
     int gcap = 1;
     for (int64_t q = 0; q < nblk; ++q) {
-      const int64_t ja = q * 256, jb = std::min(n_out, ja + 256) - 1;
-      bglo[q] = lo[ja];
-      bng[q] = lo[jb] + 2 - lo[ja];
-      gcap = std::max(gcap, (int)bng[q]);
+      const int64_t ja = q * 256, jb = std::min(n_out, ja + 256);
+      const auto mm = std::minmax_element(lo.begin() + ja, lo.begin() + jb);
+      bglo[q] = *mm.first;
+      const int64_t span = (int64_t)*mm.second + 2 - *mm.first;
+      if (span > kExactCap) {
+        bglo[q] = 0;   // lanes index the groups directly
+        bng[q] = -1;
+      } else {
+        bng[q] = (int32_t)span;
+        gcap = std::max(gcap, (int)span);
+      }
     }
     const size_t lds = (size_t)kExactBatch * gcap * sizeof(double);
-    if (lds > 160 * 1024)
-      return cleanup(), set_error("binning: a block of 256 wavelengths spans more than 5120 bins");
-    if (lds > 64 * 1024)
-      HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&bin_exact_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&bin_exact_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return cleanup(), set_error("binning: LDS opt-in failed");
     if (!x->d_hdx) {
       std::vector<double> h(std::max<int64_t>(x->nhi - 1, 1));
       for (int64_t i = 0; i + 1 < x->nhi; ++i) h[i] = (wl[i + 1] - wl[i]) * 0.5;
@@ -491,10 +535,9 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
         (rc = stage(x, 11, &d_bng, bng, st)))
       return cleanup(), rc;
     // timed: the plan uploads (pageable copies) complete first, so the events hold the kernel
-    if (x->timing) {
-      HIP_TRY(hipStreamSynchronize(st));
-      HIP_TRY(hipEventRecord(ev[0], st));
-    }
+    if (x->timing && (hipStreamSynchronize(st) != hipSuccess ||
+                      hipEventRecord(ev[0], st) != hipSuccess))
+      return cleanup(), set_error("binning: timing event failed");
     const int rows_per = std::min(U, kExactRows);
     dim3 grid((unsigned)nblk, (unsigned)((U + rows_per - 1) / rows_per));
     bin_exact_kernel<<<grid, 256, lds, st>>>(x->d_x, d_row, U, rows_per, d_s, d_e, x->d_hdx,
@@ -503,13 +546,12 @@ int bin_into(frei_xsec* x, int mode, const double* wl_bins, const double* lam, i
   }
   if (hipGetLastError() != hipSuccess) return cleanup(), set_error("binning kernel launch failed");
   if (x->timing) {
-    HIP_TRY(hipEventRecord(ev[1], st));
-    HIP_TRY(hipEventSynchronize(ev[1]));
     float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    if (hipEventRecord(ev[1], st) != hipSuccess || hipEventSynchronize(ev[1]) != hipSuccess ||
+        hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess)
+      return cleanup(), set_error("binning: timing event failed");
     x->t_ms += ms;
     x->t_n += 1;
-    for (auto e : ev) (void)hipEventDestroy(e);
   }
   if (hipStreamSynchronize(st) != hipSuccess) return cleanup(), set_error("binning kernels failed");
   cleanup();

@@ -227,3 +227,50 @@ def test_exact_binning_wavelengths_far_from_bin_centres(fa):
     ref = O.binned_opacity(xsec, T_src, p_src, wl, T_t, p_t, wl_bins, lam, False)
     assert np.isfinite(ref).all()
     assert np.array_equal(out, ref)
+
+
+def test_exact_binning_unsorted_wavelengths(fa):
+    """scipy's interp1d takes the output wavelengths in any order: a shuffled
+    wavelength grid gives each wavelength the value the sorted grid gives it — each block's LDS
+    window runs from the smallest to the largest bracket of its lanes.  Bit for bit the oracle."""
+    nu = np.linspace(1000.0, 20000.0, 200_001)
+    wl = (1e4 / nu)[1:][::-1]
+    lam0, wl_bins, _ = O.wavelength_grid(0.5, 10, 8_000)
+    rng = np.random.default_rng(15)
+    perm = rng.permutation(lam0.size)
+    lam = lam0[perm]
+    T_src, p_src = np.array([800.0, 1600.0]), np.array([1e-3, 1.0])
+    xsec = (10 ** rng.uniform(-4, 2, (2, 2, wl.size))).astype(np.float32)
+    T_t, p_t = np.array([900.0, 1500.0]), np.array([1e-2, 0.8])
+    x = fa.CrossSection(xsec, T_src, p_src, wl)
+    try:
+        out = x.bin(wl_bins, lam, T_t, p_t, groupies=False)
+        out_sorted = x.bin(wl_bins, lam0, T_t, p_t, groupies=False)
+    finally:
+        x.release()
+    ref = O.binned_opacity(xsec, T_src, p_src, wl, T_t, p_t, wl_bins, lam, False)
+    assert np.array_equal(out, ref, equal_nan=True)
+    assert np.array_equal(out, out_sorted[..., perm], equal_nan=True)
+
+
+def test_exact_binning_sparse_wavelengths_per_lane_brackets(fa):
+    """The first 300 of 60k output wavelengths skip ~100 bins each, so the first block of 256
+    spans ~25,600 bins, far more than its LDS window holds (5120): such blocks interpolate lane by lane (each lane integrates its own two
+    bins) instead of failing.  Bit for bit the oracle, mixed with dense blocks."""
+    nu = np.linspace(1000.0, 20000.0, 240_001)
+    wl = (1e4 / nu)[1:][::-1]
+    lam0, wl_bins, _ = O.wavelength_grid(0.5, 10, 60_000)
+    lam = np.concatenate([lam0[np.linspace(0, 29999, 300).astype(int)],
+                          np.linspace(lam0[30000], lam0[-1], lam0.size - 300)])
+    rng = np.random.default_rng(16)
+    T_src, p_src = np.array([800.0, 1600.0]), np.array([1e-3, 1.0])
+    xsec = (10 ** rng.uniform(-4, 2, (2, 2, wl.size))).astype(np.float32)
+    T_t, p_t = np.array([900.0, 1500.0]), np.array([1e-2, 0.8])
+    x = fa.CrossSection(xsec, T_src, p_src, wl)
+    try:
+        out = x.bin(wl_bins, lam, T_t, p_t, groupies=False)
+    finally:
+        x.release()
+    ref = O.binned_opacity(xsec, T_src, p_src, wl, T_t, p_t, wl_bins, lam, False)
+    assert np.array_equal(out, ref, equal_nan=True)
+    assert np.isfinite(ref).mean() > 0.5

@@ -2,9 +2,9 @@
 
     python tools/isa_hist.py [-DNAME=V ...] [--kernel MANGLED] [--steps-per-trip N] [--out FILE]
 
-Compiles frei_kernels.hip for gfx950 (-S, the build's flags) with FREI_ISA_E1ONLY — the E = 1
-coefficient branch and the staged partial sums compiled in unconditionally, which is the path
-every wave of the C3/C4 500k sweep takes — and walks the step loop's hot path: from the loop
+Compiles frei_kernels.hip for gfx950 (-S, the build's flags; the E = 1 coefficient head is the
+fall-through of its wave-uniform branch, the path every wave of the C3/C4 500k sweep takes) and
+walks the step loop's hot path: from the loop
 header, fall through every conditional branch (LLVM lays out the likely successor as the
 fall-through; the unlikely paths are out of line), follow unconditional ones, until the back
 edge.  One trip of the headline loop is two steps (PF = 2), i.e. two updates per lane, so the
@@ -30,7 +30,7 @@ for i, a in enumerate(sys.argv):
         outf = sys.argv[i + 1]
 asm = "/tmp/isa_hist.s"
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-ffp-contract=off",
-                "-std=c++17", "--cuda-device-only", "-S", "-Iinclude", "-DFREI_ISA_E1ONLY", *args,
+                "-std=c++17", "--cuda-device-only", "-S", "-Iinclude", *args,
                 "frei_amd/csrc/frei_kernels.hip", "-o", asm], check=True, stderr=subprocess.DEVNULL)
 s = open(asm).read()
 name = re.search(r"\n(_ZN4frei\w*" + kern + r"\w*):", s).group(1)
@@ -92,7 +92,7 @@ per = lambda n: n / steps
 mem = sum(o.startswith(("global_", "buffer_", "flat_")) for o in ops)
 lds = sum(o.startswith("ds_") for o in ops)
 lines = [f"kernel {name}  ({vgpr} VGPRs)",
-         f"defines -DFREI_ISA_E1ONLY {' '.join(args)}",
+         f"defines {' '.join(args) or '(none)'}",
          f"hot path of one loop trip ({steps} steps): {len(ops)} instructions, {len(valu)} VALU "
          f"-> {per(len(valu)):.1f} VALU per 64 updates; {per(mem):.1f} global memory and "
          f"{per(lds):.1f} LDS instructions per step",
