@@ -273,4 +273,4 @@ def test_exact_binning_sparse_wavelengths_per_lane_brackets(fa):
         x.release()
     ref = O.binned_opacity(xsec, T_src, p_src, wl, T_t, p_t, wl_bins, lam, False)
     assert np.array_equal(out, ref, equal_nan=True)
-    assert np.isfinite(ref).mean() > 0.5
+    assert np.isfinite(ref[..., :300]).all()   # the per-lane blocks are all finite values
