@@ -76,6 +76,7 @@ SIGNATURES = {
     "frei_contract_timing": (ctypes.c_int, [_vp, _dp, _dp]),
     "frei_graph_info": (ctypes.c_int, [_vp, _ip, _ip]),
     "frei_chain_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64)]),
+    "frei_tail_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64)]),
     "frei_comm_shared_device": (ctypes.c_int, [_vp, ctypes.c_int]),
     "frei_device_pci_bus_id": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
     "frei_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),

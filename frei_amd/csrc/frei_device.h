@@ -289,6 +289,12 @@ struct FastArgs {
   int* ch_err;                          // set to 1 when a wait gave up
   // the deferred update's output temperatures: block 0 fills them with kPoisonT (nullptr: none)
   double* poison;
+  // Trailing update (sweep_pipe_tail_kernel, round 6): the sweep blocks publish each phase's
+  // per-block partial sums into tail_part as soon as the phase is done (write-through stores,
+  // every slot kPoisonT until then), so the launch's trailing update workgroups can start a
+  // layer's reduction while the sweep is still in flight (nullptr: partials into `part` at the
+  // end, as every other form)
+  double* tail_part;
 };
 // "not yet published" pattern of a chained temperature: a signalling NaN, which no arithmetic
 // produces (results are quiet NaNs), so a diverged run's NaN temperature is still a value
@@ -367,6 +373,12 @@ struct UpdateArgs {
   // (layer converged) (nullptr: a launch of its own)
   unsigned long long* epoch;
   unsigned long long epoch_val;
+  // trailing update in the sweep's own launch (sweep_pipe_tail_kernel): the partials are polled
+  // until no slot holds kPoisonT (each 8-byte value is its own ready flag), bounded by
+  // poll_timeout wall_clock64 ticks, after which *poll_err is set and the value is used as is
+  int poll;
+  long long poll_timeout;
+  int* poll_err;
 };
 
 // LDS bytes of the update kernel (K4/K5): T, dT, p, T before/after absorb, ln p ratios,
@@ -412,6 +424,14 @@ void launch_sweep_fast_chain(int dir, int depth, int pf, const FastArgs& a, cons
 // phases ahead
 void launch_sweep_pipe(int dir, int NC, int PF, const FastArgs& a, int nblocks, hipStream_t st);
 size_t pipe_lds_bytes(int NC, int M, int ns);
+// The producer/consumer sweep (NC = 4) with its fused update u as n_tail trailing workgroups of
+// the same launch (u.poll: the update polls each phase's partials as the sweep publishes them
+// into a.tail_part; the trailing workgroups refill `clear` — the previous launch's partials —
+// with kPoisonT).  nbx sweep blocks; single atmosphere.
+void launch_sweep_pipe_tail(int dir, int PF, const FastArgs& a, const UpdateArgs& u, int nbx,
+                            int n_tail, double* clear, hipStream_t st);
+size_t pipe_tail_lds_bytes(int ns, int n_tnodes);
+void launch_poison(double* x, int64_t n, hipStream_t st);
 void launch_nan_scan(const double* x, int64_t n, int* flag, hipStream_t st);
 void launch_reduce(const double* part, int nblocks, double* Fb, int n_idx, const int* conv,
                    int force, hipStream_t st, int n_atm = 1, int64_t part_stride = 0,

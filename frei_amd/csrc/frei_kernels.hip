@@ -1550,7 +1550,7 @@ __host__ __device__ inline int64_t pipe_lds_doubles(int NC, int M, int ns) {
          (int64_t)NC * ns * 4 + (int64_t)ns * kStepDoubles;
 }
 
-template <int DIR, int NC, int M, int PF, bool CH>
+template <int DIR, int NC, int M, int PF, bool CH, bool TL = false>
 __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __restrict__ ss,
                                                 double* __restrict__ Fu, double* __restrict__ Fd,
                                                 double* __restrict__ part,
@@ -1612,9 +1612,30 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
     if (conv0) return;   // block-uniform, ahead of the barrier
     __syncthreads();
   }
-  TRACE_MARK(1);
+  if constexpr (!TL) TRACE_MARK(1);
   auto rslot = [&](int ph, int s, int v) {
     return ring + ((((ph & 1) * G + s) * kPipeNV + v) << 6) + lane;
+  };
+  // TL (trailing update): right after the barrier that ends phase q + 1, wave 0 (a producer) sums
+  // phase q's staged partials over the NC consumers — the order of the end-of-sweep epilogue
+  // below, so the values are bitwise its — and publishes them by write-through stores into slots
+  // that hold kPoisonT until then: the trailing update workgroups start on a layer as soon as
+  // every block has published its steps, while the sweep runs on.  Step-major, [steps x 4][nbx]:
+  // an update slot's 256 threads read one value of 64 consecutive blocks per load instruction
+  // (block-major, each lane's load was a line of its own: 8k line requests per CU and poll pass,
+  // ~4-7 us under the sweep's traffic, profiles/r06/tail/).
+  auto publish = [&](int q) {
+    if constexpr (TL) {
+      const int idx = q * G * 4 + lane;
+      if (wv == 0 && q >= 0 && lane < G * 4 && idx < ns * 4) {
+        double v = red[idx];
+        for (int w = 1; w < NC; ++w) v += red[(int64_t)w * ns * 4 + idx];
+        __hip_atomic_store((gu64*)(a.tail_part + (int64_t)idx * nbx + bx),
+                           __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (q == 0) TRACE_MARK(1);   // (trace builds: phase 0 published)
+    }
   };
   if (role < kPipeP) {
     // ---------------- producer
@@ -1703,15 +1724,18 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
       for (int ph = 0; ph <= nph; ph += 2) {   // nph + 1 barriers, like the consumer's
         produce(ph, b0);
         __syncthreads();
+        publish(ph - 1);
         if (ph + 1 <= nph) {
           produce(ph + 1, b1);
           __syncthreads();
+          publish(ph);
         }
       }
     } else {
       for (int ph = 0; ph <= nph; ++ph) {
         produce(ph, b0);
         __syncthreads();
+        publish(ph - 1);
       }
     }
   } else {
@@ -1799,13 +1823,15 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
     }
   }
   TRACE_MARK(2);
-  __syncthreads();
-  for (int idx = tid; idx < ns * 4; idx += 256 * NC) {
-    double s = red[idx];
-    for (int w = 1; w < NC; ++w) s += red[(int64_t)w * ns * 4 + idx];
-    part[part_at(idx, bx, nbx, ns * 4)] = s;
+  if constexpr (!TL) {   // (TL: every phase is already published)
+    __syncthreads();
+    for (int idx = tid; idx < ns * 4; idx += 256 * NC) {
+      double s = red[idx];
+      for (int w = 1; w < NC; ++w) s += red[(int64_t)w * ns * 4 + idx];
+      part[part_at(idx, bx, nbx, ns * 4)] = s;
+    }
   }
-  TRACE_PUT(CH ? 50 + NC : 20 + NC);
+  TRACE_PUT(CH ? 50 + NC : TL ? 60 + NC : 20 + NC);
 }
 
 template <int DIR, int NC, int M, int PF>
@@ -1864,8 +1890,13 @@ size_t pipe_lds_bytes(int NC, int M, int ns) {
 // release fence orders the value stores before the flag stores for any observer; the
 // explicit wait keeps the compiler from dropping the fence's completion wait (gfx950 hazard,
 // MI355X_MICROARCH.md "Compiler hazard").
+// release = false (the trailing update, which pushes while its own launch's sweep is running):
+// no fence — a system-scope release writes back the XCD L2's dirty lines (MI355X_MICROARCH.md:
+// ~6.5 µs with freshly dirtied data), and during a sweep the L2 holds the flux rows it is
+// writing; the payload is system-scope write-through stores, completed by the wait below before
+// any flag store, the "sc0 sc1 stores and loads both sides" form.
 __device__ __forceinline__ void p2p_push_values(const P2PPush& p, int64_t idx, const double* v,
-                                                int nv) {
+                                                int nv, bool release = true) {
   const int par = (int)(p.seq & 1);
   for (int r = 0; r < p.nranks; ++r) {
     uint64_t* dst = reinterpret_cast<uint64_t*>(p.peers[r] + mbox_val(par, p.rank, p.nranks, p.n));
@@ -1873,7 +1904,7 @@ __device__ __forceinline__ void p2p_push_values(const P2PPush& p, int64_t idx, c
       __hip_atomic_store(dst + idx + k, __builtin_bit_cast(uint64_t, v[k]), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   // The system-scope release orders the value stores before the flag stores for any observer.
   // (The payload is only the write-through system-scope stores above, so the completion wait
   // alone would order them too; without the fence: measured no different,
@@ -2340,6 +2371,11 @@ __device__ __forceinline__ void update_arrive(const UpdateArgs& a, int nU, int i
   __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifdef FREI_TAIL_POLL_SYS
+#define FREI_POLL_SCOPE __HIP_MEMORY_SCOPE_SYSTEM
+#else
+#define FREI_POLL_SCOPE __HIP_MEMORY_SCOPE_AGENT
+#endif
 // Layer lr of nU update workgroups, run by kRedThreads threads (tid) — part h of a 512- or
 // 1024-thread block in a chained launch (each part its own LDS: sh, and the [h] arrays below).  A
 // half past the last layer (lr >= n_layers, odd layer counts) computes the last layer again
@@ -2634,6 +2670,340 @@ void launch_sweep_pipe_chain(int dir, int PF, const FastArgs& a, const UpdateArg
     if (dir == kEmit) go(sweep_pipe_chain_kernel<kEmit, 1>);
     else go(sweep_pipe_chain_kernel<kAbsorb, 1>);
   }
+}
+
+// ---------------------------------------------------------------- trailing update (round 6)
+// The producer/consumer sweep (four consumers per block) with its own fused update as trailing
+// workgroups of the same launch: blocks [0, nbx) sweep and publish each phase's partial sums as
+// soon as the phase is done (sweep_pipe_body<TL>); blocks [nbx, nbx + nT) each run four
+// 256-thread update slots over the layers in the order the sweep finishes them, slot h of block t
+// in round r taking position (r nT + t) 4 + h (emit: layer = position; absorb: n_layers - 1 -
+// position).  A layer's reduction waits only for the steps it reads (twostream.py:396-407: dT_l
+// needs layer l's four bolometric sums), so all but the last layers' updates run while the
+// sweep is still in flight, and the next sweep waits for one kernel boundary instead of two.
+// Forward progress: the sweep blocks wait for nothing; the update blocks come after them in
+// dispatch order (launched only while the device has a free CU per update block, so they are
+// resident beside the sweep) and wait only for sweep blocks of their own launch and, over P2P,
+// for the other ranks' update blocks.  The update blocks also put the previous launch's
+// partials (`clear`, the other of two buffers) back to kPoisonT for the next launch, by
+// write-through stores (a plain store would leave the line in this XCD's L2, where the next
+// launch's polls of it would find the stale kPoisonT).
+//
+// One layer of the update (tail_update_slot): update_fused_body's computation in the same
+// order — the same summation tree over the sweep blocks (thread t adds blocks t, t + 256, ...;
+// the xor butterfly per wave; the waves in order), the same layer_dT of layers l and l + 1, the
+// same bookkeeping and the same step record — restricted to the case the trailing update serves
+// (one atmosphere, contracted table with shared brackets, fixed mixing ratios, fused exchange)
+// and ordered so that only the partial sums are live while they are polled: the 128 VGPRs of a
+// 16-wave block hold it without spills (update_fused_body, which loads every input up front,
+// spilled 544 B per lane here and took 3-5x its standalone time, profiles/r06/tail/).
+// A trailing block's copy of every per-layer input of the update, loaded once at its start (none
+// of them is written in the launch by anyone but the layer's own slot): the slots' dT and
+// bookkeeping then wait on no global load (round 6: loading them after the poll put three
+// dependent global round trips, ~5 us, behind every layer's sums).
+struct TailIn {
+  double *T, *p, *Tb, *Ta, *mmr, *nodes;
+  int *flips, *prev, *nd;
+  PMeta* pm;
+  LayerPre* pre;   // [n_layers] layer_pre of every layer (formed at the block's start)
+};
+__host__ __device__ inline size_t tail_in_bytes(int nL, int ntn) {
+  return (size_t)nL * (sizeof(PMeta) + sizeof(LayerPre)) + (size_t)(5 * nL + ntn) * sizeof(double) +
+         (size_t)3 * nL * sizeof(int);
+}
+__device__ __forceinline__ TailIn tail_in_layout(double* lds, int nL, int ntn) {
+  TailIn t;
+  t.pre = reinterpret_cast<LayerPre*>(lds);
+  t.pm = reinterpret_cast<PMeta*>(t.pre + nL);
+  double* d = reinterpret_cast<double*>(t.pm + nL);
+  t.T = d;
+  t.p = d + nL;
+  t.Tb = d + 2 * nL;
+  t.Ta = d + 3 * nL;
+  t.mmr = d + 4 * nL;
+  t.nodes = d + 5 * nL;
+  int* q = reinterpret_cast<int*>(t.nodes + ntn);
+  t.flips = q;
+  t.prev = q + nL;
+  t.nd = q + 2 * nL;
+  return t;
+}
+
+#ifdef FREI_TRACE
+__shared__ unsigned long long g_tail_done[4];
+__shared__ unsigned g_tail_pass[4];
+#endif
+__device__ __forceinline__ void tail_update_slot(const UpdateArgs& a, int lr, int tid, int h,
+                                                 double (&wsum)[kRedWaves][8],
+                                                 const TailIn& in, int conv, int it) {
+  TRACE_DECL;
+  const int nL = a.su.n_layers;
+  const bool on = lr < nL;
+  const int l = on ? lr : nL - 1;
+  const int dir = a.dir;
+  const int k0 = layer_step(dir, l, nL);
+  const int k1 = l + 1 < nL ? layer_step(dir, l + 1, nL) : -1;
+  const bool skip = !a.force && conv;   // converged: the sweep published nothing
+  const bool sums = !skip && (k0 >= 0 || k1 >= 0);
+  const int nb = a.nblocks;   // <= 256 (a trailing launch leaves free CUs)
+  // ---- thread t polls sweep block t's partial sums of steps k0 (values 0..3) and k1 (4..7),
+  // then update_fused_body's tree: the xor butterfly per wave, the waves in order (a block t +
+  // 256, ... never exists here)
+  if (sums) {
+    const double* pj[8];
+    for (int j = 0; j < 8; ++j) {
+      const int k = (j < 4) ? (k0 >= 0 ? k0 : k1) : (k1 >= 0 ? k1 : k0);
+      pj[j] = a.part + (int64_t)(k * 4 + (j & 3)) * nb;
+    }
+    const int b = min(tid, nb - 1);
+    unsigned long long x[8];
+    auto load_all = [&]() {
+      bool m = false;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        x[j] = __hip_atomic_load((const gu64*)(pj[j] + b), __ATOMIC_RELAXED, FREI_POLL_SCOPE);
+        m |= x[j] == kPoisonT;
+      }
+      return m;
+    };
+    bool miss = load_all();
+#ifdef FREI_TRACE
+    int passes = 1;
+#endif
+    if (__any(miss)) {
+      const long long t0 = wall_clock64();
+      do {   // (every value re-read each pass: no data-dependent load)
+        __builtin_amdgcn_s_sleep(1);
+        miss = load_all();
+#ifdef FREI_TRACE
+        ++passes;
+#endif
+        if (__any(miss) && (wall_clock64() - t0 > a.poll_timeout ||
+                            __hip_atomic_load(a.poll_err, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT))) {
+          __hip_atomic_store(a.poll_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      } while (__any(miss));
+    }
+#ifdef FREI_TRACE
+    // the slot's last poll to finish, and the most passes any lane needed (trace builds)
+    atomicMax(&g_tail_done[h], (unsigned long long)wall_clock64());
+    atomicMax(&g_tail_pass[h], (unsigned)passes);
+#endif
+    double acc[8];
+    for (int j = 0; j < 8; ++j) acc[j] = tid < nb ? 0.0 + __builtin_bit_cast(double, x[j]) : 0.0;
+    for (int j = 0; j < 8; ++j) acc[j] = butterfly_sum(acc[j], tid & 63);
+    if ((tid & 63) == 0)
+      for (int j = 0; j < 8; ++j) wsum[tid >> 6][j] = acc[j];
+  }
+  __syncthreads();
+  TRACE_MARK(2);
+#ifdef FREI_TRACE
+  if (sums) {   // the block's last poll (over its four slots) and the most passes
+    unsigned long long dm = 0;
+    unsigned pm = 0;
+    for (int q = 0; q < 4; ++q) dm = max(dm, g_tail_done[q]), pm = max(pm, g_tail_pass[q]);
+    tr_[1] = (long long)(dm & ((1ull << 40) - 1)) | ((long long)pm << 40);
+  }
+  __syncthreads();
+  if (tid == 0) g_tail_done[h] = 0, g_tail_pass[h] = 0;
+#endif
+  if (skip) {   // carry T into the output buffer
+    if (tid == 0 && on) publish_T(a, l, in.T[l], conv, true);
+    return;
+  }
+  // this rank's sums in wave order (lanes 0..7: k0's four, then k1's)
+  auto own = [&](int q) {
+    double t = wsum[0][q];
+    for (int w = 1; w < kRedWaves; ++w) t += wsum[w][q];
+    return t;
+  };
+  if (a.p2p.mbox && tid == 64 && k0 >= 0 && on) {   // push while wave 0 waits for the peers
+    double t4[4];
+    for (int q = 0; q < 4; ++q) t4[q] = own(q);
+    p2p_push_values(a.push, (int64_t)k0 * 4, t4, 4, false);
+  }
+  if (tid >= 64) return;
+  const int li = min(l + (tid & 1), nL - 1);
+  const int kd = (tid & 1) ? k1 : k0;
+  double v = 0.0;
+  const int k = tid < 4 ? k0 : k1;
+  if (tid < 8 && k >= 0) {
+    v = own(tid);
+    if (a.p2p.mbox) {   // all ranks' sums in rank order (own rank from registers)
+      const double mine = v;
+      const int64_t idx = (int64_t)k * 4 + (tid & 3);
+      const long long t0 = wall_clock64();
+      for (int r = 0; r < a.p2p.nranks; ++r)
+        if (r != a.push.rank) p2p_wait(a.p2p, r, idx, t0);
+      for (int r = 0; r < a.p2p.nranks; ++r) {
+        const double xr = (r == a.push.rank) ? mine : p2p_value(a.p2p, r, idx);
+        v = (r == 0) ? xr : v + xr;
+      }
+    }
+  }
+  const int base = (tid & 1) * 4;
+  double F[4];
+  for (int q = 0; q < 4; ++q) F[q] = __shfl(v, base + q, 64);
+  if (tid < 4 && k0 >= 0 && a.bol_out && on) a.bol_out[(int64_t)l * 4 + tid] = v;
+  // dT of layers l (lane 0) and l + 1 (lane 1): layer_dT's expressions
+  const double T1 = in.T[li];
+  double d = 0.0;
+  if (tid < 2 && kd >= 0) d = layer_dT_post(F, in.pre[li]);
+  const double Tn = T1 - d;               // lane 0: layer l, lane 1: layer l + 1
+  const double Tn1 = __shfl(Tn, 1, 64);   // layer l + 1's new temperature (lane 0)
+  if (tid != 0 || !on) return;
+  // layer l's bookkeeping (update_kernel's expressions)
+  const double dT = d;
+  const double Tnew = Tn;
+  if (a.dT_out) a.dT_out[l] = dT;
+  bool c = true;
+  if (a.track) {
+    if (dir == kEmit) {
+      a.Tb[l] = Tnew;
+    } else {
+      const double Tb = in.Tb[l], Ta = in.Ta[l];
+      int flips = in.flips[l], prev = in.prev[l], nd = in.nd[l];
+      if (it < a.hist_cap) {
+        a.hist[((int64_t)it * 2 + 0) * nL + l] = Tb;
+        a.hist[((int64_t)it * 2 + 1) * nL + l] = Tnew;
+      }
+      const double d0 = Tb - Ta, d1 = Tnew - Tb;
+      for (int q = (it > 0 ? 0 : 1); q < 2; ++q) {
+        const double dd = q == 0 ? d0 : d1;
+        const int sgn = (dd > 0) - (dd < 0);
+        if (nd > 0 && sgn != prev) ++flips;
+        prev = sgn;
+        ++nd;
+      }
+      a.flips[l] = flips;
+      a.prev_sign[l] = prev;
+      a.ndiff[l] = nd;
+      a.Ta[l] = Tnew;
+      c = (flips > a.n_zero_crossings) || (fabs(dT) < a.convergence_dT);
+    }
+  }
+  publish_T(a, l, Tnew, conv, c);
+  update_arrive(a, nL, it, !c);
+  // the next sweep's step record of layer l (setup_sweep's shared-bracket record, S = 1)
+  const int kn = a.next_dir >= 0 ? layer_step(a.next_dir, l, nL) : -1;
+  if (kn >= 0) {
+    const int tp = (a.next_dir == kEmit && l == nL - 1) ? 1 : 0;
+    FastStepS f{};
+    f.layer = l;
+    f.top = tp;
+    f.iT1 = 1.0 / Tnew;
+    f.iT2 = tp ? f.iT1 : 1.0 / Tn1;
+    const double p2 = tp ? a.su.p_top2 : in.p[l + 1];
+    f.dm = (in.p[l] - p2) / a.su.g;
+    int64_t off;
+    double wlo, whi;
+    fast_term(a.su.spec[0], in.pm[l], in.nodes, Tnew, off, wlo, whi);
+    f.off = off;
+    f.wlo = wlo;
+    f.whi = whi;
+    for (int q = 0; q < kMaxFastS; ++q) f.mmr[q] = q < 1 ? in.mmr[l] : 0.0;
+    a.su.ssteps[kn] = f;
+  }
+  TRACE_PUT(31);
+}
+
+template <int DIR, int PF>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
+void sweep_pipe_tail_kernel(FastArgs a, UpdateArgs u, const FastStepS* __restrict__ ss,
+                            double* __restrict__ Fu, double* __restrict__ Fd,
+                            double* __restrict__ dtaus, double* __restrict__ clear,
+                            int64_t n_clear) {
+  static_assert(kRedThreads == 256, "update slots of 256 threads");
+  extern __shared__ double lds[];
+  const int nbx = u.nblocks;
+  if ((int)blockIdx.x < nbx) {
+    sweep_pipe_body<DIR, 4, 2, PF, false, true>(a, ss, Fu, Fd, nullptr, dtaus, lds, blockIdx.x,
+                                                nbx);
+    return;
+  }
+  __shared__ double wsum[4][kRedWaves][8];
+  const int t = blockIdx.x - nbx, nT = gridDim.x - nbx;
+  const int nL = u.su.n_layers, ntn = u.su.n_tnodes;
+  const int tid = threadIdx.x;
+  const TailIn in = tail_in_layout(lds, nL, ntn);
+  // every per-layer input once (issued before the refill below, which waits on nothing)
+  for (int q = tid; q < nL; q += 1024) {
+    const double Tq = u.su.T[q], pq = u.su.p[q];
+    in.T[q] = Tq;
+    in.p[q] = pq;
+    in.mmr[q] = u.su.mmr[q];
+    // dT's flux-independent part of layer q (layer_dT's first half, update_fused_body's inputs)
+    const bool top = (u.dir == kEmit && q == nL - 1);
+    const int q1 = min(q + 1, nL - 1);
+    in.pre[q] = layer_pre(Tq, top ? Tq : u.su.T[q1], pq, top ? u.su.p_top2 : u.su.p[q1], u.lnp[q],
+                          u.su.g, u.m_bar, u.alpha);
+    in.pm[q] = u.su.pmeta[q];
+    if (u.track) {
+      in.Tb[q] = u.Tb[q];
+      in.Ta[q] = u.Ta[q];
+      in.flips[q] = u.flips[q];
+      in.prev[q] = u.prev_sign[q];
+      in.nd[q] = u.ndiff[q];
+    }
+  }
+  for (int q = tid; q < ntn; q += 1024) in.nodes[q] = u.su.tnodes[q];
+  const int conv = *u.conv, it = *u.iter;
+  // the previous launch's partials back to "not published" (write-through: see above)
+  for (int64_t i = (int64_t)t * 1024 + tid; i < n_clear; i += (int64_t)nT * 1024)
+    __hip_atomic_store((gu64*)clear + i, kPoisonT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int h = tid >> 8;
+  for (int r = 0;; ++r) {
+    const int p0 = (r * nT + t) * 4;
+    if (p0 >= nL) break;
+    const int p = p0 + h;
+    const int lr = p >= nL ? nL : (u.dir == kEmit ? p : nL - 1 - p);
+    tail_update_slot(u, lr, tid & 255, h, wsum[h], in, conv, it);
+    __syncthreads();   // the next round's slots rewrite wsum and the stage
+  }
+}
+
+size_t pipe_tail_lds_bytes(int ns, int n_tnodes) {
+  return std::max(pipe_lds_bytes(4, 2, ns), tail_in_bytes(ns + 1, n_tnodes));
+}
+
+void launch_sweep_pipe_tail(int dir, int PF, const FastArgs& a, const UpdateArgs& u,
+                            int nbx, int n_tail, double* clear, hipStream_t st) {
+  const size_t shm = pipe_tail_lds_bytes(a.n_steps, u.su.n_tnodes);
+  const int64_t n_clear = (int64_t)nbx * a.n_steps * 4;
+  auto go = [&](auto kernel) {
+    static std::unordered_map<const void*, size_t> optin;
+    size_t& have = optin[reinterpret_cast<const void*>(kernel)];
+    if (shm > have) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      have = shm;
+    }
+    hipLaunchKernelGGL(kernel, dim3(nbx + n_tail), dim3(1024), shm, st, a, u, a.ssteps, a.F_up,
+                       a.F_down, a.dtaus, clear, n_clear);
+  };
+  if (PF == 2) {
+    if (dir == kEmit) go(sweep_pipe_tail_kernel<kEmit, 2>);
+    else go(sweep_pipe_tail_kernel<kAbsorb, 2>);
+  } else {
+    if (dir == kEmit) go(sweep_pipe_tail_kernel<kEmit, 1>);
+    else go(sweep_pipe_tail_kernel<kAbsorb, 1>);
+  }
+}
+
+// Fill n 8-byte slots with kPoisonT ("not published"): the trailing update's partial buffers
+// (write-through stores: no copy of the line stays in this XCD's L2 for a later poll to find).
+__global__ void poison_kernel(unsigned long long* x, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    __hip_atomic_store((gu64*)x + i, kPoisonT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+void launch_poison(double* x, int64_t n, hipStream_t st) {
+  const int nb = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(poison_kernel, dim3(nb > 0 ? nb : 1), dim3(256), 0, st,
+                     reinterpret_cast<unsigned long long*>(x), n);
 }
 
 // The one-lane form chained (contracted single table, step records formed in the block).

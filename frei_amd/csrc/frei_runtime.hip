@@ -135,6 +135,16 @@ struct frei_ctx {
   std::vector<uint64_t> g_key;
   int g_captures = 0, g_replays = 0;     // frei_graph_info
   int64_t n_chained = 0;                // chained sweep launches so far (frei_chain_info)
+  // Trailing update (FREI_TAIL, round 6): the producer/consumer sweep's launch carries its own
+  // fused update as trailing workgroups that reduce each layer as soon as the sweep has
+  // published its steps (launch_sweep_pipe_tail).  Two partial-sum buffers used alternately:
+  // a launch publishes into one and its update workgroups put the other back to kPoisonT.
+  int tail = 1;                         // FREI_TAIL: 1 when it applies, 0 off
+  double* d_tpart = nullptr;            // [2][tpart_n]
+  int64_t tpart_n = 0;
+  int tpart_parity = 0;
+  bool tpart_fill = true;               // both buffers must be (re)filled with kPoisonT
+  int64_t n_tail = 0;                   // trailing-update launches so far (frei_tail_info)
   bool shared_device = false;           // ranks share this GPU: no chained launches
   std::vector<uint64_t>* keys = nullptr;  // collecting run_sweep's argument hashes
   bool dry = false;                       // run_sweep computes hashes only (no launches)
@@ -754,6 +764,24 @@ bool chain_ready(frei_ctx* c) {
   return c->chain == 2 && c->prefetch_depth != 1;
 }
 
+// Update workgroups of a trailing-update launch (0: not used): the producer/consumer sweep with
+// four consumers, the fused update (one atmosphere, local or P2P exchange), stream launches
+// without per-sweep events (they would time the update with the sweep), not chained, ranks not
+// sharing the device, and — so that they are resident beside the sweep, never waiting behind
+// it — at least two CUs left free by the sweep's one block per CU (eight update blocks at most).
+int tail_blocks(const frei_ctx* c, int nb_sweep) {
+  if (!(c->tail && c->fast && c->eff && c->shared && c->n_atm == 1 && !c->use_graph && !c->keys &&
+        !c->timing && !c->shared_device && !c->chem_on))
+    return 0;
+  if (!(c->fused_update && !c->comm && !(c->nranks > 1 && c->host_ag) &&
+        (2 * (size_t)c->nL + c->tnodes.size()) * sizeof(double) <= 32 * 1024))
+    return 0;
+  if (pipe_consumers(c) != 4 || records_in_sweep(const_cast<frei_ctx*>(c))) return 0;
+  if (pipe_tail_lds_bytes(c->nL - 1, (int)c->tnodes.size()) + 6 * 1024 > c->lds_optin) return 0;
+  const int free_cu = c->n_cu - nb_sweep;
+  return free_cu >= 2 ? std::min(free_cu, 8) : 0;
+}
+
 // Launch a deferred update on its own (the next sweep cannot take it, or the caller needs its
 // results now).  Its output buffer holds kPoisonT until the update writes it.
 int flush_update(frei_ctx* c) {
@@ -845,6 +873,8 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
     HIP_TRY(hipEventRecord(e0, c->stream));
   }
   int nb_run = c->nblocks;  // partial-sum columns written by this sweep
+  FastArgs tail_f{};        // a trailing-update launch: the sweep's arguments (launched below)
+  int tail_nT = 0;          // its update workgroups (0: not a trailing-update launch)
   const bool rec_on = c->fast && records_in_sweep(c);
   // a sweep that reads the update's records after one whose update skipped them (an option or
   // the tables changed mid-run): write this sweep's records first
@@ -910,6 +940,8 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
       c->has_pend = false;
       launch_sweep_pipe_chain(o.dir, c->pipe_pf, f, u, nb_run, c->stream);
       ++c->n_chained;
+    } else if (NC > 0 && (tail_nT = tail_blocks(c, nb_run)) > 0) {
+      tail_f = f;   // launched with its update (which needs the P2P arguments below)
     } else if (NC > 0) {
       launch_sweep_pipe(o.dir, NC, c->pipe_pf, f, nb_run, c->stream);
     } else if (Q > 1 && merge) {
@@ -1043,6 +1075,30 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
     if (defer_own) {   // runs at the head of the next sweep's launch, or flush_update
       c->pend = u;
       c->has_pend = true;
+    } else if (tail_nT > 0) {   // the sweep and this update in one launch
+      const int64_t need = (int64_t)nb_run * ns * 4;
+      if (c->tpart_n < need) {
+        dfree(c->d_tpart);
+        c->tpart_n = 0;
+        TRY(dalloc(&c->d_tpart, 2 * (size_t)need));
+        c->tpart_n = need;
+        c->tpart_fill = true;
+      }
+      if (c->tpart_fill) {
+        launch_poison(c->d_tpart, 2 * c->tpart_n, c->stream);
+        c->tpart_fill = false;
+        c->tpart_parity = 0;
+      }
+      double* cur = c->d_tpart + c->tpart_parity * c->tpart_n;
+      double* other = c->d_tpart + (1 - c->tpart_parity) * c->tpart_n;
+      c->tpart_parity ^= 1;
+      tail_f.tail_part = cur;
+      u.part = cur;
+      u.poll = 1;
+      u.poll_timeout = (long long)(c->p2p_timeout_s * 1e8);   // wall_clock64: 100 MHz
+      u.poll_err = c->d_chain_err;
+      launch_sweep_pipe_tail(o.dir, c->pipe_pf, tail_f, u, nb_run, tail_nT, other, c->stream);
+      ++c->n_tail;
     } else if (!c->dry) {
       launch_update_fused(u, c->stream);
     }
@@ -1113,7 +1169,7 @@ const char* const kOptionNames[] = {"prefetch_depth", "shared", "shared_max_bloc
                                     "quad_max_blocks", "red_rows", "red_stage", "group_q",
                                     "fused_update", "graph", "pipe", "pipe_pf", "pipe_min_blocks", "rec_sweep",
                                     "pipe_max_blocks", "prefetch_steps", "k7_mfma", "sweep_lds_kb", "group_waves", "chain",
-                                    "lam2", nullptr};
+                                    "lam2", "tail", nullptr};
 int set_option(frei_ctx* c, const std::string& k, int v) {
   if (k == "prefetch_depth") c->prefetch_depth = v;
   else if (k == "shared") c->shared_mode = v < 0 ? -1 : (v ? 1 : 0);
@@ -1136,6 +1192,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "group_waves") c->group_waves = v == 8 ? 8 : 4;
   else if (k == "chain") c->chain = v < 0 ? 0 : (v > 2 ? 2 : v);
   else if (k == "lam2") c->lam2 = v < 0 ? -1 : (v ? 1 : 0);
+  else if (k == "tail") c->tail = v != 0;
   else if (k == "sweep_lds_kb") c->sweep_lds_kb = v < 0 ? 0 : (v > 160 ? 160 : v);
   else if (k == "prefetch_steps") c->prefetch_steps = v >= 16 ? 16 : v >= 8 ? 8 : v == 2 ? 2 : 0;
   else return fail("unknown option '" + k + "'");
@@ -1150,7 +1207,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
 // idle right before a timed loop (bench.py's warm-up synchronize) and changed how the power
 // management clocked the loop that followed (profiles/r04/bisect/README.md).
 int check_comm(frei_ctx* c) {
-  const bool chain = c->d_chain_err && c->n_chained != c->chain_checked;
+  const bool chain = c->d_chain_err && c->n_chained + c->n_tail != c->chain_checked;
   const bool comm = c->d_comm_err != nullptr;
   if (!chain && !comm) return 0;
   if (chain)
@@ -1160,13 +1217,15 @@ int check_comm(frei_ctx* c) {
     HIP_TRY(hipMemcpyAsync(&c->h_err[1], c->d_comm_err, sizeof(int), hipMemcpyDeviceToHost,
                            c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  c->chain_checked = c->n_chained;
+  c->chain_checked = c->n_chained + c->n_tail;
   if (chain && c->h_err[0]) {   // reported once: rearm it so later runs are not failed by it
     drop_pending(c);
+    c->tpart_fill = true;       // a trailing update gave up: its buffers are in no known state
     c->h_err[0] = 0;
     HIP_TRY(hipMemsetAsync(c->d_chain_err, 0, sizeof(int), c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    return fail("chained sweep: the update workgroups never published the temperatures");
+    return fail("chained sweep / trailing update: a wait for values another workgroup "
+                "publishes gave up (FREI_P2P_TIMEOUT_S)");
   }
   if (comm && c->h_err[1])
     return fail("P2P exchange timed out: a peer rank did not publish its partial sums "
@@ -1304,6 +1363,7 @@ int frei_ctx_destroy(frei_ctx* c) {
   dfree(c->d_wait_ticks);
   dfree(c->d_epoch);
   dfree(c->d_chain_err);
+  dfree(c->d_tpart);
   for (auto& s : c->sp) dfree(s.d_tab);
   dfree(c->d_eff);
   dfree(c->d_smeta_eff);
@@ -1817,6 +1877,12 @@ int frei_device_pci_bus_id(int device, char* buf, int len) {
   return 0;
 }
 
+int frei_tail_info(frei_ctx* c, int64_t* launches) {
+  if (!c || !launches) return fail("null argument");
+  *launches = c->n_tail;
+  return 0;
+}
+
 int frei_chain_info(frei_ctx* c, int64_t* chained) {
   if (!c || !chained) return fail("null argument");
   *chained = c->n_chained;
@@ -2237,7 +2303,9 @@ int frei_ctx_path(frei_ctx* c, int* flags) {
   const bool lam2 = c->fast && m.lam2;
   *flags = (c->fast ? 1 : 0) | (c->fast && c->shared ? 2 : 0) | (c->eff ? 4 : 0) |
            (nan ? 8 : 0) | (NC == 0 && Q == 2 ? 16 : 0) | (NC == 0 && Q == 4 ? 32 : 0) |
-           (NC << 6) | (lam2 ? 512 : 0);
+           (NC << 6) | (lam2 ? 512 : 0) |
+           (c->fast && NC > 0 && !chain_ready(c) && tail_blocks(c, (int)((c->nlam + 255) / 256)) > 0
+                ? 1024 : 0);
   return 0;
 }
 

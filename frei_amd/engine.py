@@ -412,7 +412,7 @@ class Engine:
         v = f.value
         return dict(fast=bool(v & 1), lds_steps=bool(v & 2), contracted=bool(v & 4),
                     nan=bool(v & 8), paired=bool(v & 16), quad=bool(v & 32),
-                    pipe=(v >> 6) & 7, lam2=bool(v & 512))
+                    pipe=(v >> 6) & 7, lam2=bool(v & 512), tail=bool(v & 1024))
 
     def set_option(self, name, value):
         """Tuning knob of include/frei_hip.h frei_set_option (e.g. "precontract", 0)."""
@@ -423,6 +423,13 @@ class Engine:
         cap, rep = ctypes.c_int(0), ctypes.c_int(0)
         N.check(N.lib().frei_graph_info(self._ctx, ctypes.byref(cap), ctypes.byref(rep)))
         return cap.value, rep.value
+
+    def tail_count(self):
+        """Trailing-update launches so far (frei_tail_info): producer/consumer sweeps whose
+        launch also ran their own fused update, layer by layer as the sweep published them."""
+        n = ctypes.c_int64(0)
+        N.check(N.lib().frei_tail_info(self._ctx, ctypes.byref(n)))
+        return n.value
 
     def chain_count(self):
         """Chained sweep launches so far (frei_chain_info): sweeps whose launch also ran the

@@ -221,7 +221,9 @@ int frei_contribution(frei_ctx* ctx, const double* dtaus, const double* nu,
  * hold NaN (per-species nansum variant), bit 4 / bit 5 grouped-lane sweep with two / four
  * lanes per wavelength (small slices), bits 6-8: consumer waves per block of the
  * producer/consumer sweep (1, 2 or 4; 0 = not used), bit 9 two wavelengths per lane in the
- * contracted one-lane sweep (large slices: option "lam2"). */
+ * contracted one-lane sweep (large slices: option "lam2"), bit 10 the producer/consumer sweep
+ * runs its update as trailing workgroups of its own launch (option "tail"; loops without
+ * per-sweep events). */
 int frei_ctx_path(frei_ctx* ctx, int* flags);
 
 /* Tuning knobs (also FREI_<NAME> in the environment at context creation): "precontract"
@@ -231,7 +233,10 @@ int frei_ctx_path(frei_ctx* ctx, int* flags);
  * "red_rows", "red_stage" (take effect at the next metadata build), "fused_update" (1: one
  * launch for the partial-sum reduction and the T update when the exchange is local or P2P;
  * 0: two kernels; bitwise identical results; takes effect at the next sweep), "graph" (1:
- * replay T-P iterations from a captured hipGraph; 0, the default: launch kernel by kernel). */
+ * replay T-P iterations from a captured hipGraph; 0, the default: launch kernel by kernel),
+ * "tail" (1, the default: the producer/consumer sweep's fused update runs as trailing
+ * workgroups of the sweep's launch, layer by layer as the sweep publishes; 0: a launch of its
+ * own after the sweep; bitwise identical results). */
 int frei_set_option(frei_ctx* ctx, const char* name, int value);
 /* With the "graph" option on (default off), T-P iterations (frei_iterate, frei_run) are
  * replayed from a captured hipGraph of a few iterations when one rank runs with timing off:
@@ -241,6 +246,12 @@ int frei_graph_info(frei_ctx* ctx, int* captures, int* replays);
  * workgroups run the previous sweep's deferred fused update).  Never while per-sweep HIP events
  * are on (frei_timing) or when P2P ranks share this device. */
 int frei_chain_info(frei_ctx* ctx, int64_t* chained);
+/* Trailing-update launches so far (FREI_TAIL / option "tail", round 6): producer/consumer sweeps
+ * whose launch also ran their own fused update, layer by layer as the sweep published each
+ * layer's partial sums (twostream.py:396-407: a layer's dT needs only its own four bolometric
+ * sums), instead of a separate update kernel after the sweep.  Never while per-sweep HIP events
+ * are on, when chained, or when ranks share this device; bitwise the separate launches. */
+int frei_tail_info(frei_ctx* ctx, int64_t* launches);
 /* Ranks of this communicator share the context's GPU (shared != 0): no chained launches (a
  * chained launch's sweep blocks spin on update workgroups that wait for every rank's sums, and
  * could hold the CUs another rank's kernels need).  frei_amd sets it when two ranks report the
