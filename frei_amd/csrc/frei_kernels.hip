@@ -2885,7 +2885,12 @@ __device__ __forceinline__ void tail_update_slot(const UpdateArgs& a, int lr, in
     }
   }
   publish_T(a, l, Tnew, conv, c);
-  update_arrive(a, nL, it, !c);
+  // update_arrive's convergence AND, its atomic's round trip overlapped with the record below
+  const bool arrive = a.track && dir == kAbsorb;
+  unsigned old = 0;
+  if (arrive)
+    old = __hip_atomic_fetch_add(a.done, 1u + (!c ? 65536u : 0u), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
   // the next sweep's step record of layer l (setup_sweep's shared-bracket record, S = 1)
   const int kn = a.next_dir >= 0 ? layer_step(a.next_dir, l, nL) : -1;
   if (kn >= 0) {
@@ -2905,6 +2910,12 @@ __device__ __forceinline__ void tail_update_slot(const UpdateArgs& a, int lr, in
     f.whi = whi;
     for (int q = 0; q < kMaxFastS; ++q) f.mmr[q] = q < 1 ? in.mmr[l] : 0.0;
     a.su.ssteps[kn] = f;
+  }
+  if (arrive && (old & 0xffffu) == (unsigned)nL - 1) {   // the last layer in
+    const unsigned nc = (old >> 16) + (!c ? 1u : 0u);
+    *a.iter = it + 1;
+    if (nc == 0 && a.stop_on_conv) *a.conv = 1;
+    __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   TRACE_PUT(31);
 }

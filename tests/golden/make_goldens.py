@@ -18,6 +18,9 @@ Cases (file -> reference functions exercised):
   c1_step1.npz      Grid.emission_spectrum(n_timesteps=1), example opacity + gray variant (core.py:233-338)
   c1_converge.npz   Grid.emission_spectrum(n_timesteps=100) to convergence
   c2small.npz       60 x 2048, 2 species separable T-varying tables (16 T nodes), 3 iterations
+  c2strong.npz      c2small's grid and line forests at 1e3x strength, clipped to [10, 1e3]
+                    cm^2 g^-1: a well-conditioned twin (the reference algorithm's one-ulp floor
+                    3e-13, against c2small's 2.4e-10), held to 1e-10 outright (round 6)
   c1_vmr3e4.npz     test_core.py:19-71's Grid (example opacity, n_timesteps=1) with kappa's
                     chemistry a constant VMR of 3e-4 -- the H2O maximum FastChem gives in the
                     reference's CI (test_chemistry.py:45-46), which reproduces its pins
@@ -337,6 +340,32 @@ def case_c2small():
     o, _, _, _ = spectrum_case(g, 3, "")
     out.update(o)
     save("c2small.npz", **out)
+
+
+def case_c2strong():
+    """c2small's Grid and line forests, 1e3 times stronger and clipped to [10, 1e3]: no layer is
+    optically thin, so the reference's own one-ulp floor is 3e-13 (c2small: 2.4e-10) and a 1e-10
+    comparison needs no floor rule."""
+    pl = planet()
+    g = R.core.Grid(pl, n_wl_bins=2048, n_layers=60, T_ref=1500 * u.K)
+    lam = g.lam.to(u.um).value
+    pb = g.pressures.to(u.bar).value
+    Tmin, Tmax = g.init_temperatures.value.min(), g.init_temperatures.value.max()
+    T_nodes = np.linspace(0.8 * Tmin, 1.2 * Tmax, 16)
+    out = dict(lam=lam, pressures=pb, init_temperatures=g.init_temperatures.value,
+               T_nodes=T_nodes, clip_lo=10.0, clip_hi=1e3)
+    tabs = {}
+    for s, name in enumerate(["1H2-16O", "12C-16O"]):
+        base, fp, fT = separable_table(np.random.default_rng(42 + s), lam, pb, T_nodes)
+        base = base * 1e3
+        out[f"s{s}_base"], out[f"s{s}_fp"], out[f"s{s}_fT"] = base, fp, fT
+        tabs[name] = R.DataArray(build_table(base, fp, fT, lo=10.0, hi=1e3),
+                                 dims=["pressure", "temperature", "wavelength"],
+                                 coords=dict(pressure=pb, temperature=T_nodes, wavelength=lam))
+    g.load_opacities(opacities=tabs)
+    o, _, _, _ = spectrum_case(g, 3, "")
+    out.update(o)
+    save("c2strong.npz", **out)
 
 
 def vmr_chemistry(vmr):

@@ -92,6 +92,33 @@ def grid_floor(spectrum, up, down, spectrum_1ulp, up_1ulp, down_1ulp):
             row_normwise(down_1ulp, down))
 
 
+# The well-conditioned twin of every test family whose entries may pass through the floor rule
+# (ill-conditioned inputs: optically thin layers, many non-converged iterations): a test of the
+# same path on inputs whose one-ulp floor is far below 1e-10, held to 1e-10 outright.  Every
+# logged entry names its rule, and a floor-rule entry its twin;
+# tests/test_host.py checks that each twin exists.
+OUTRIGHT_TWINS = {
+    "test_batched_atmospheres_match_oracle_per_atmosphere":
+        "tests/test_gpu_batch.py::test_batched_atmospheres_strong_opacity_at_1e10_outright",
+    "test_reference_binned_tables_drop_in_by_dimension_name":
+        "tests/test_gpu_boundary.py::test_reference_binned_strong_table_at_1e10",
+    "test_grid_feeds_the_provider_to_radiative_equilibrium":
+        "tests/test_gpu_chemistry_provider.py::test_provider_radiative_equilibrium_at_1e10_outright",
+    "test_c2small_two_species_matches_reference":
+        "tests/test_gpu_parity.py::test_c2strong_two_species_matches_reference_outright",
+    "test_temperature_dependent_chemistry_matches_oracle":
+        "tests/test_gpu_parity.py::test_temperature_dependent_chemistry_matches_oracle[c1_strong]",
+    "test_high_albedo_lanes_match_oracle":
+        "tests/test_gpu_parity.py::test_high_albedo_lanes_match_oracle[1--2]",
+}
+
+
+def outright_twin(test_id):
+    """The OUTRIGHT_TWINS entry of a pytest node id (its function name, parameters dropped)."""
+    name = test_id.split("::")[-1].split("[")[0]
+    return OUTRIGHT_TWINS.get(name)
+
+
 # Observed grid-level errors of every assert_grid_parity call in this session (test name, the
 # measured errors, the one-ulp floor and the tolerance applied); tests/conftest.py writes them
 # to $FREI_PARITY_JSON at the end of the session (committed as profiles/r03/parity.json).
@@ -138,6 +165,9 @@ def assert_grid_parity(spectrum, ref_spectrum, up=None, ref_up=None, down=None, 
     entry["within_1e-10"] = all(entry[k] <= RTOL for k in
                                 ("spectrum_elementwise", "F_up_rownorm", "F_down_rownorm",
                                  "T_elementwise") if k in entry)
+    entry["rule"] = "1e-10" if entry["within_1e-10"] else "2x the one-ulp floor"
+    if not entry["within_1e-10"]:
+        entry["outright_twin"] = outright_twin(entry["test"])
     entry["passed"] = not fails
     PARITY_LOG.append(entry)
     assert not fails, f"{what}: " + "; ".join(fails)

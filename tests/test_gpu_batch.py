@@ -79,6 +79,51 @@ def test_batched_atmospheres_match_oracle_per_atmosphere(fa, monkeypatch, k7_mfm
                            floor, T=out["final_T"][m], ref_T=oT, T_floor=T_floor)
 
 
+def test_batched_atmospheres_strong_opacity_at_1e10_outright(fa):
+    """The well-conditioned twin of the toy batched atmospheres above: five
+    atmospheres on tables of 10-1000 cm^2 g^-1 (no optically thin layer; seed chosen so that no
+    layer sits on the convective branch's switch), four fixed T-P iterations through K7 and the
+    batched sweeps, each atmosphere against its own oracle run at 1e-10 with no floor rule —
+    the reference algorithm's own one-ulp floor here is <= 1.3e-13, asserted too."""
+    rng = np.random.default_rng(30)
+    names = ["1H2-16O", "12C-16O", "Na"]
+    lam, _, _ = O.wavelength_grid(0.5, 10, 2048)
+    nL = 30
+    p = O.pressure_grid(nL, -6, np.log10(200))
+    Tn = np.linspace(400.0, 5000.0, 12)
+    tabs_o, tabs_f = {}, {}
+    for n in names:
+        base = 10 ** rng.uniform(0, 4.5, lam.size)
+        fp, fT = (p / 1.0) ** 0.1, (Tn / 1000.0) ** 0.5
+        tabs_o[n] = O.Table(O.separable_table(base, fp, fT, 10.0, 1e3), p, Tn)
+        tabs_f[n] = fa.SeparableTable(base, fp, fT, p, Tn, lo=10.0, hi=1e3)
+    T_ref = rng.uniform(1100, 2500, 5)
+    g = rng.uniform(800.0, 6000.0, 5)
+    mh = rng.uniform(-0.5, 1.0, 5)
+    mmr0 = O.mock_mmr(names, M_BAR)
+    mmr = np.array([(mmr0 * 10 ** m)[:, None] * np.ones(nL) for m in mh])
+    T0 = np.array([O.temperature_grid(p, t, 0.1, 0.1) for t in T_ref])
+    Ft = O.F_TOA(lam)
+    eng = fa.BatchEngine(lam, p, tabs_f, g=g, mmr=mmr, F_toa=Ft)
+    try:
+        assert eng.path()["contracted"]
+        out = eng.run(T0, n_timesteps=4, n_zero_crossings=10 ** 6, convergence_dT=-1.0, alpha=1.0)
+        ups, downs = eng.get_fluxes()
+    finally:
+        eng.close()
+    for m in range(5):
+        run = lambda: O.emission_spectrum(tabs_o, T0[m], p, lam, Ft, g[m], M_BAR, 1,
+                                          n_timesteps=4, n_zero_crossings=10 ** 6,
+                                          convergence_dT=-1.0, mmr=mmr[m])
+        osp, oT, oth, odt, ou, od, it = run()
+        with perturbed_exp():
+            psp, pT, _, _, pu, pd, _ = run()
+        assert max(grid_floor(osp, ou, od, psp, pu, pd)) < 1e-12 and rel(pT, oT) < 1e-12
+        e = assert_grid_parity(out["spectra"][m], osp, ups[m], ou, downs[m], od,
+                               f"strong atmosphere {m} (outright)", T=out["final_T"][m], ref_T=oT)
+        assert e["within_1e-10"], e
+
+
 @pytest.mark.parametrize("k7_mfma", ["1", "0"])
 def test_batched_mfma_contraction_tiles_and_padding(fa, monkeypatch, k7_mfma):
     """17 atmospheres (two 16-row MFMA tiles, one padded) x 5 species (a padded K step):

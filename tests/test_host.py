@@ -167,3 +167,23 @@ def test_chemistry_provider_called_on_the_reference_signature():
     import pytest
     with pytest.raises(KeyError, match="12C-1H4"):
         C.provider_mmr(fake, [1000.0], [1.0], names + ["12C-1H4"], 4e-24)
+
+
+def test_every_floor_family_names_an_existing_outright_twin():
+    """tests/parity.py OUTRIGHT_TWINS: each floor-rule test family names a well-conditioned twin
+    held to 1e-10 outright; the twin's test function (and the parameter id, where one is named)
+    exists in the tree."""
+    import ast
+    import pathlib
+    import re
+    from tests.parity import OUTRIGHT_TWINS
+    root = pathlib.Path(__file__).resolve().parents[1]
+    for family, twin in OUTRIGHT_TWINS.items():
+        path, node = twin.split("::")
+        src = (root / path).read_text()
+        fn = node.split("[")[0]
+        funcs = {n.name for n in ast.walk(ast.parse(src)) if isinstance(n, ast.FunctionDef)}
+        assert fn in funcs, twin
+        assert re.search(rf"def {family}\(", (root / "tests").joinpath(
+            next(p.name for p in (root / "tests").glob("test_gpu_*.py")
+                 if f"def {family}(" in p.read_text())).read_text()), family
