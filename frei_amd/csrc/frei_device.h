@@ -253,6 +253,12 @@ struct SetupArgs {
   FastStepS* ssteps;       // [n_layers - 1] (fast path, shared brackets)
   int shared;              // all species share p and T nodes
   AtmStride bs;            // batched atmospheres (blockIdx.x of setup/update kernels)
+  // Lazy K3 (round 6): [n_p * n_T] 1 where the contracted row (pressure row, T node) holds
+  // its values (nullptr: the whole table was contracted up front).  Records written from T get
+  // the mask of their two rows not yet contracted in off[1] (bit 0: T_lo row, bit 1: T_hi row);
+  // an update marks the rows the sweep before it used.  kpitch: the tables' row pitch.
+  int32_t* kvalid;
+  int64_t kpitch;
 };
 
 struct FastArgs {
@@ -289,6 +295,12 @@ struct FastArgs {
   int* ch_err;                          // set to 1 when a wait gave up
   // the deferred update's output temperatures: block 0 fills them with kPoisonT (nullptr: none)
   double* poison;
+  // Lazy K3 (sweep_pair_kernel): a step whose record masks rows not yet contracted (off[1])
+  // contracts them for the lane's own wavelengths first — K3's sum, same order — into tab[0]
+  // (kmmr == nullptr: every row is contracted)
+  const double* ktab[kMaxFastS];
+  const double* kmmr;      // [n_species][n_layers]
+  int kS, kNL;
   // Trailing update (sweep_pipe_tail_kernel, round 6): the sweep blocks publish each phase's
   // per-block partial sums into tail_part as soon as the phase is done (write-through stores,
   // every slot kPoisonT until then), so the launch's trailing update workgroups can start a

@@ -1329,7 +1329,30 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
   auto layer_of = [&](int k) { return step_layer(DIR, k, ns + 1); };
   auto top_of = [&](int k) { return DIR == kEmit && k == ns - 1; };
   auto clampk = [&](int k) { return k < ns ? k : ns - 1; };
+  // lazy K3: the rows a record masks (off[1], wave-uniform) are contracted here for this lane's
+  // two wavelengths first — contract_kernel's sum, species in order — then read back by the
+  // same lane (no other lane or block reads them in this launch)
+  auto contract_rows = [&](const FastStep& sk) {
+    const int64_t mask = sk.off[1];
+    const int l = sk.layer;
+    for (int b = 0; b < 2; ++b) {
+      if (!(mask & (1 << b))) continue;
+      const int64_t o = sk.off[0] + b * a.pitch + j;
+      d2 acc = ld2(a.ktab[0] + o);
+      acc = d2{a.kmmr[l] * acc.x, a.kmmr[l] * acc.y};
+#pragma unroll
+      for (int s = 1; s < kMaxFastS; ++s) {   // (static indices: the arguments stay in SGPRs)
+        if (s < a.kS) {
+          const d2 v = ld2(a.ktab[s] + o);
+          const double m = a.kmmr[(int64_t)s * a.kNL + l];
+          acc = d2{acc.x + m * v.x, acc.y + m * v.y};
+        }
+      }
+      st2(const_cast<double*>(a.tab[0]) + o, acc);
+    }
+  };
   auto load_rows = [&](int k, d2 (&v)[2], double dep1 = 0.0, double dep2 = 0.0) {
+    if (a.kmmr && st[clampk(k)].off[1]) contract_rows(st[clampk(k)]);   // (rare, uniform)
     const double* r = a.tab[0] + after_use(st[clampk(k)].off[0] + j, dep1, dep2);
     v[0] = ld2(r);
     v[1] = ld2(r + a.pitch);
@@ -2076,7 +2099,7 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
       const int k = kb + idx / kMaxFastS, s = idx % kMaxFastS;
       FastStep* f = u.fsteps + k;
       if (s >= nS) {
-        f->off[s] = 0;
+        if (!(u.kvalid && s == 1)) f->off[s] = 0;   // (lazy K3: off[1] is species 0's mask)
         f->wlo[s] = f->whi[s] = f->mmr[s] = 0.0;
         continue;
       }
@@ -2088,6 +2111,14 @@ __device__ void setup_sweep(const SetupArgs& u, const double* T, const double* P
       f->wlo[s] = wlo;
       f->whi[s] = whi;
       f->mmr[s] = MMR(s, i);
+      if (u.kvalid && s == 0) {   // lazy K3 (contracted table, nS = 1): rows still to contract
+        int64_t mask = 0;
+        if (wlo != 0.0 || whi != 0.0) {   // (outside the hull: zero weights on row 0, zeroed)
+          const int64_t r = off / u.kpitch;
+          mask = (u.kvalid[r] ? 0 : 1) | (u.kvalid[r + 1] ? 0 : 2);
+        }
+        f->off[1] = mask;
+      }
     }
     return;
   }
@@ -2574,6 +2605,19 @@ __device__ void update_fused_body(const UpdateArgs& a, int lr, int nU, int tid, 
   }
   TRACE_MARK(2);
   __syncthreads();   // sTn of layers l, l + 1
+  if (a.su.kvalid && tid == 64 && on && k0 >= 0) {
+    // lazy K3: the sweep that just ran contracted every row its records masked, so layer l's
+    // rows at the temperature that sweep used (T_in) are complete now; marked by the thread
+    // that forms layer l's next record below (it reads them back in program order)
+    int64_t off;
+    double wlo, whi;
+    fast_term(rSp, rPm, sNodes, Tl, off, wlo, whi);   // (thread 64: species 0, layer l)
+    if (wlo != 0.0 || whi != 0.0) {
+      const int64_t r = off / a.su.kpitch;
+      a.su.kvalid[r] = 1;
+      a.su.kvalid[r + 1] = 1;
+    }
+  }
   if (kn >= 0 && tid >= 64 && on) {
     if (stage)
       setup_sweep(a.su, sTn, sP, sNodes, sSp, sPm, sMm, a.next_dir, kn, kn + 1, tid - 64,

@@ -174,6 +174,15 @@ struct frei_ctx {
   // FREI_PRECONTRACT=0 keeps the per-species sum inside the sweep.
   int eff = 0, eff_mode = -1;
   double* d_eff = nullptr;
+  // Lazy K3 (FREI_LAZY_K3, round 6): with the two-wavelength sweep, the setup contracts no row;
+  // a sweep contracts the rows its records mask as missing (the lane's own wavelengths), and the
+  // update after it marks them (d_kvalid).  A run touches a fraction of the table's T nodes (C3
+  // to radiative equilibrium: 191 of 960 rows).  Any other sweep form first contracts the
+  // whole table (eff_complete).
+  int lazy_k3 = 1;
+  bool lazy_on = false;
+  bool eff_complete = true;
+  int32_t* d_kvalid = nullptr;
   size_t eff_cap = 0;
   SpecMeta* d_smeta_eff = nullptr;
   double* d_ones = nullptr;
@@ -354,9 +363,13 @@ bool lam2_static(const frei_ctx* c, int depth, int pf) {
          pf <= 2 && c->red_stage && staged_sums_fit(c->nL - 1);
 }
 
+bool lam2_form(const frei_ctx* c);   // (below: fast_form)
+
 template <typename Lap>
 int build_contracted(frei_ctx* c, bool shared_fast, Lap&& lap) {
   const int nL = c->nL, S = c->S;
+  c->lazy_on = false;        // (decided below, with the contracted table)
+  c->eff_complete = true;
   const bool batch = c->n_atm > 1;
   // (a T-dependent chemistry changes mmr every sweep: the species sum stays in the sweep)
   bool on = shared_fast && (S >= 2 || batch) && (c->eff_mode != 0 || batch) && !c->chem_on;
@@ -429,6 +442,26 @@ int build_contracted(frei_ctx* c, bool shared_fast, Lap&& lap) {
   TRY(h2d(c->d_prow, prow.data(), nL, c->stream));
   const double* tabs[kMaxFastS];
   for (int s = 0; s < S; ++s) tabs[s] = c->sp[s].d_tab;
+  // lazy K3: the sweeps that read this table take two wavelengths per lane (the form run_sweep
+  // launches for a loop's sweeps), one atmosphere
+  c->lazy_on = c->lazy_k3 && !batch && lam2_form(c);
+  c->eff_complete = !c->lazy_on;
+  if (c->lazy_on) {
+    dfree(c->d_kvalid);
+    TRY(dalloc(&c->d_kvalid, (size_t)q0.n_p * q0.n_T));
+    HIP_TRY(hipMemsetAsync(c->d_kvalid, 0, (size_t)q0.n_p * q0.n_T * sizeof(int32_t),
+                           c->stream));
+    // a layer outside the hull reads rows 0 and 1 with zero weights: finite (zero) until then
+    HIP_TRY(hipMemsetAsync(c->d_eff, 0, 2 * (size_t)q0.stride * sizeof(double), c->stream));
+    c->contract_ms = 0.0;
+    c->contract_bytes = 0.0;
+    lap(4);
+    SpecMeta m = c->smeta[0];
+    m.tab = c->d_eff;
+    if (!c->d_smeta_eff) TRY(dalloc(&c->d_smeta_eff, 1));
+    TRY(h2d(c->d_smeta_eff, &m, 1, c->stream));
+    return 0;
+  }
   hipEvent_t k0 = nullptr, k1 = nullptr;   // the contraction kernel alone (frei_contract_timing)
   if (hipEventCreate(&k0) != hipSuccess || hipEventCreate(&k1) != hipSuccess)
     return fail("hipEventCreate failed");
@@ -669,6 +702,8 @@ SetupArgs setup_args(frei_ctx* c) {
   u.ssteps = c->d_ssteps;
   u.shared = c->shared;
   u.bs = atm_stride(c);
+  u.kvalid = c->lazy_on ? c->d_kvalid : nullptr;
+  u.kpitch = c->sp.empty() ? 0 : c->sp[0].stride;
   if (c->chem_on) {
     u.chem.tab = c->d_chem_tab;
     u.chem.T = c->d_chem_T;
@@ -832,6 +867,31 @@ FastForm fast_form(const frei_ctx* c, bool merge) {
   return m;
 }
 
+bool lam2_form(const frei_ctx* c) { return fast_form(c, false).lam2; }
+
+// Lazy K3: contract every row not contracted yet (any sweep form other than the two-wavelength
+// one, which contracts its masked rows itself, or an update that does not mark them).
+int complete_contraction(frei_ctx* c) {
+  if (c->eff_complete) return 0;
+  const Species& q0 = c->sp[0];
+  const double* tabs[kMaxFastS];
+  for (int s = 0; s < c->S; ++s) tabs[s] = c->sp[s].d_tab;
+  std::vector<int32_t> prow(c->nL);
+  for (int l = 0; l < c->nL; ++l) {
+    const PMeta& pm = c->pmeta[l];
+    prow[l] = (pm.wp_lo != 0.0) ? pm.p_lo : pm.p_hi;
+  }
+  launch_contract(tabs, c->S, c->d_mmr, c->d_prow, c->nL, q0.n_T, q0.stride, c->d_eff, c->stream);
+  HIP_TRY(hipGetLastError());
+  std::vector<int32_t> ones((size_t)q0.n_p * q0.n_T, 0);
+  for (int l = 0; l < c->nL; ++l)
+    for (int t = 0; t < q0.n_T; ++t) ones[(size_t)prow[l] * q0.n_T + t] = 1;
+  TRY(h2d(c->d_kvalid, ones.data(), ones.size(), c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));   // (the host vector)
+  c->eff_complete = true;
+  return 0;
+}
+
 // One sweep: K1 -> fused reduce + update (+ next setup; P2P exchange inside), or K1 ->
 // reduce -> [RCCL / host all-gather] -> K4/K5 (batched contexts, RCCL, host hook,
 // fused_update 0).  Asynchronous.
@@ -896,9 +956,19 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
     f.wtr = c->d_wtr;
     f.ftoa = c->d_ftoa;
     const FastForm m = fast_form(c, merge);
+    // lazy K3: only the two-wavelength sweep with the fused update (which marks the rows it
+    // used) contracts on the way; any other form gets the whole table first
+    if (c->lazy_on && !c->eff_complete && !c->dry && !(m.lam2 && fused_ok(c)))
+      TRY(complete_contraction(c));
     const int S_run = m.S_run;
     for (int q = 0; q < kMaxFastS; ++q) f.tab[q] = q < c->S ? c->sp[q].d_tab : nullptr;
     if (c->eff) f.tab[0] = c->d_eff;
+    if (c->lazy_on && !c->eff_complete) {   // the two-wavelength sweep contracts masked rows
+      for (int q = 0; q < kMaxFastS; ++q) f.ktab[q] = q < c->S ? c->sp[q].d_tab : nullptr;
+      f.kmmr = c->d_mmr;
+      f.kS = c->S;
+      f.kNL = c->nL;
+    }
     f.steps = c->d_fsteps;
     f.ssteps = c->d_ssteps;
     f.F_up = c->d_Fu;
@@ -1079,6 +1149,7 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
       const int64_t need = (int64_t)nb_run * ns * 4;
       if (c->tpart_n < need) {
         dfree(c->d_tpart);
+  dfree(c->d_kvalid);
         c->tpart_n = 0;
         TRY(dalloc(&c->d_tpart, 2 * (size_t)need));
         c->tpart_n = need;
@@ -1169,7 +1240,7 @@ const char* const kOptionNames[] = {"prefetch_depth", "shared", "shared_max_bloc
                                     "quad_max_blocks", "red_rows", "red_stage", "group_q",
                                     "fused_update", "graph", "pipe", "pipe_pf", "pipe_min_blocks", "rec_sweep",
                                     "pipe_max_blocks", "prefetch_steps", "k7_mfma", "sweep_lds_kb", "group_waves", "chain",
-                                    "lam2", "tail", nullptr};
+                                    "lam2", "tail", "lazy_k3", nullptr};
 int set_option(frei_ctx* c, const std::string& k, int v) {
   if (k == "prefetch_depth") c->prefetch_depth = v;
   else if (k == "shared") c->shared_mode = v < 0 ? -1 : (v ? 1 : 0);
@@ -1193,6 +1264,7 @@ int set_option(frei_ctx* c, const std::string& k, int v) {
   else if (k == "chain") c->chain = v < 0 ? 0 : (v > 2 ? 2 : v);
   else if (k == "lam2") c->lam2 = v < 0 ? -1 : (v ? 1 : 0);
   else if (k == "tail") c->tail = v != 0;
+  else if (k == "lazy_k3") c->lazy_k3 = v != 0;
   else if (k == "sweep_lds_kb") c->sweep_lds_kb = v < 0 ? 0 : (v > 160 ? 160 : v);
   else if (k == "prefetch_steps") c->prefetch_steps = v >= 16 ? 16 : v >= 8 ? 8 : v == 2 ? 2 : 0;
   else return fail("unknown option '" + k + "'");
@@ -2305,7 +2377,8 @@ int frei_ctx_path(frei_ctx* c, int* flags) {
            (nan ? 8 : 0) | (NC == 0 && Q == 2 ? 16 : 0) | (NC == 0 && Q == 4 ? 32 : 0) |
            (NC << 6) | (lam2 ? 512 : 0) |
            (c->fast && NC > 0 && !chain_ready(c) && tail_blocks(c, (int)((c->nlam + 255) / 256)) > 0
-                ? 1024 : 0);
+                ? 1024 : 0) |
+           (c->lazy_on ? 2048 : 0);
   return 0;
 }
 

@@ -412,7 +412,8 @@ class Engine:
         v = f.value
         return dict(fast=bool(v & 1), lds_steps=bool(v & 2), contracted=bool(v & 4),
                     nan=bool(v & 8), paired=bool(v & 16), quad=bool(v & 32),
-                    pipe=(v >> 6) & 7, lam2=bool(v & 512), tail=bool(v & 1024))
+                    pipe=(v >> 6) & 7, lam2=bool(v & 512), tail=bool(v & 1024),
+                    lazy_k3=bool(v & 2048))
 
     def set_option(self, name, value):
         """Tuning knob of include/frei_hip.h frei_set_option (e.g. "precontract", 0)."""

@@ -223,7 +223,8 @@ int frei_contribution(frei_ctx* ctx, const double* dtaus, const double* nu,
  * producer/consumer sweep (1, 2 or 4; 0 = not used), bit 9 two wavelengths per lane in the
  * contracted one-lane sweep (large slices: option "lam2"), bit 10 the producer/consumer sweep
  * runs its update as trailing workgroups of its own launch (option "tail"; loops without
- * per-sweep events). */
+ * per-sweep events), bit 11 lazy K3: the setup contracted no row, the two-wavelength sweeps
+ * contract the rows their records reach first (option "lazy_k3"). */
 int frei_ctx_path(frei_ctx* ctx, int* flags);
 
 /* Tuning knobs (also FREI_<NAME> in the environment at context creation): "precontract"
@@ -236,7 +237,10 @@ int frei_ctx_path(frei_ctx* ctx, int* flags);
  * replay T-P iterations from a captured hipGraph; 0, the default: launch kernel by kernel),
  * "tail" (1, the default: the producer/consumer sweep's fused update runs as trailing
  * workgroups of the sweep's launch, layer by layer as the sweep publishes; 0: a launch of its
- * own after the sweep; bitwise identical results). */
+ * own after the sweep; bitwise identical results), "lazy_k3" (1, the default: with the
+ * two-wavelength sweep, K3 contracts no row at setup — each sweep contracts the (pressure row,
+ * T node) rows its records reach for the first time, for its own wavelengths, with K3's sum;
+ * 0: every row at setup; bitwise identical results). */
 int frei_set_option(frei_ctx* ctx, const char* name, int value);
 /* With the "graph" option on (default off), T-P iterations (frei_iterate, frei_run) are
  * replayed from a captured hipGraph of a few iterations when one rank runs with timing off:
