@@ -2896,7 +2896,28 @@ __device__ __forceinline__ void tail_update_slot(const UpdateArgs& a, int lr, in
   double d = 0.0;
   if (tid < 2 && kd >= 0) d = layer_dT_post(F, in.pre[li]);
   const double Tn = T1 - d;               // lane 0: layer l, lane 1: layer l + 1
-  const double Tn1 = __shfl(Tn, 1, 64);   // layer l + 1's new temperature (lane 0)
+  const double Tl0 = __shfl(Tn, 0, 64);   // layer l's new temperature (lane 1)
+  // lane 1: the next sweep's step record of layer l (setup_sweep's shared-bracket record, S = 1)
+  // while lane 0 does the bookkeeping and the convergence arrival (round trips in parallel)
+  const int kn = a.next_dir >= 0 ? layer_step(a.next_dir, l, nL) : -1;
+  if (tid == 1 && on && kn >= 0) {
+    const int tp = (a.next_dir == kEmit && l == nL - 1) ? 1 : 0;
+    FastStepS f{};
+    f.layer = l;
+    f.top = tp;
+    f.iT1 = 1.0 / Tl0;
+    f.iT2 = tp ? f.iT1 : 1.0 / Tn;
+    const double p2 = tp ? a.su.p_top2 : in.p[l + 1];
+    f.dm = (in.p[l] - p2) / a.su.g;
+    int64_t off;
+    double wlo, whi;
+    fast_term(a.su.spec[0], in.pm[l], in.nodes, Tl0, off, wlo, whi);
+    f.off = off;
+    f.wlo = wlo;
+    f.whi = whi;
+    for (int q = 0; q < kMaxFastS; ++q) f.mmr[q] = q < 1 ? in.mmr[l] : 0.0;
+    a.su.ssteps[kn] = f;
+  }
   if (tid != 0 || !on) return;
   // layer l's bookkeeping (update_kernel's expressions)
   const double dT = d;
@@ -2929,38 +2950,7 @@ __device__ __forceinline__ void tail_update_slot(const UpdateArgs& a, int lr, in
     }
   }
   publish_T(a, l, Tnew, conv, c);
-  // update_arrive's convergence AND, its atomic's round trip overlapped with the record below
-  const bool arrive = a.track && dir == kAbsorb;
-  unsigned old = 0;
-  if (arrive)
-    old = __hip_atomic_fetch_add(a.done, 1u + (!c ? 65536u : 0u), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-  // the next sweep's step record of layer l (setup_sweep's shared-bracket record, S = 1)
-  const int kn = a.next_dir >= 0 ? layer_step(a.next_dir, l, nL) : -1;
-  if (kn >= 0) {
-    const int tp = (a.next_dir == kEmit && l == nL - 1) ? 1 : 0;
-    FastStepS f{};
-    f.layer = l;
-    f.top = tp;
-    f.iT1 = 1.0 / Tnew;
-    f.iT2 = tp ? f.iT1 : 1.0 / Tn1;
-    const double p2 = tp ? a.su.p_top2 : in.p[l + 1];
-    f.dm = (in.p[l] - p2) / a.su.g;
-    int64_t off;
-    double wlo, whi;
-    fast_term(a.su.spec[0], in.pm[l], in.nodes, Tnew, off, wlo, whi);
-    f.off = off;
-    f.wlo = wlo;
-    f.whi = whi;
-    for (int q = 0; q < kMaxFastS; ++q) f.mmr[q] = q < 1 ? in.mmr[l] : 0.0;
-    a.su.ssteps[kn] = f;
-  }
-  if (arrive && (old & 0xffffu) == (unsigned)nL - 1) {   // the last layer in
-    const unsigned nc = (old >> 16) + (!c ? 1u : 0u);
-    *a.iter = it + 1;
-    if (nc == 0 && a.stop_on_conv) *a.conv = 1;
-    __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  update_arrive(a, nL, it, !c);
   TRACE_PUT(31);
 }
 
