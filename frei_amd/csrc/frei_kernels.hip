@@ -1792,8 +1792,21 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
         if (act) {
           const bool st_up = (DIR == kEmit) ? !top : (!a.live_only || layer == 0);
           const bool st_dn = (DIR == kAbsorb) || !a.live_only || top;
-          if (st_up) store_flux(Fu + (int64_t)(layer + 1) * nl + j, F2u);
-          if (st_dn) store_flux(Fd + (int64_t)layer * nl + j, F1d);
+          if constexpr (TL) {
+            // write-through: the XCDs' L2s then hold no dirty flux lines while the trailing
+            // update's P2P push makes its system-scope release (a writeback of this XCD's L2)
+            if (st_up)
+              __hip_atomic_store((gu64*)(Fu + (int64_t)(layer + 1) * nl + j),
+                                 __builtin_bit_cast(unsigned long long, F2u), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+            if (st_dn)
+              __hip_atomic_store((gu64*)(Fd + (int64_t)layer * nl + j),
+                                 __builtin_bit_cast(unsigned long long, F1d), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            if (st_up) store_flux(Fu + (int64_t)(layer + 1) * nl + j, F2u);
+            if (st_dn) store_flux(Fd + (int64_t)layer * nl + j, F1d);
+          }
         }
         double* t = t0 + ((k & 1) * 4) * kStageRow + lane;
         t[0] = wt * F2u;
@@ -1913,13 +1926,8 @@ size_t pipe_lds_bytes(int NC, int M, int ns) {
 // release fence orders the value stores before the flag stores for any observer; the
 // explicit wait keeps the compiler from dropping the fence's completion wait (gfx950 hazard,
 // MI355X_MICROARCH.md "Compiler hazard").
-// release = false (the trailing update, which pushes while its own launch's sweep is running):
-// no fence — a system-scope release writes back the XCD L2's dirty lines (MI355X_MICROARCH.md:
-// ~6.5 µs with freshly dirtied data), and during a sweep the L2 holds the flux rows it is
-// writing; the payload is system-scope write-through stores, completed by the wait below before
-// any flag store, the "sc0 sc1 stores and loads both sides" form.
 __device__ __forceinline__ void p2p_push_values(const P2PPush& p, int64_t idx, const double* v,
-                                                int nv, bool release = true) {
+                                                int nv) {
   const int par = (int)(p.seq & 1);
   for (int r = 0; r < p.nranks; ++r) {
     uint64_t* dst = reinterpret_cast<uint64_t*>(p.peers[r] + mbox_val(par, p.rank, p.nranks, p.n));
@@ -1927,7 +1935,7 @@ __device__ __forceinline__ void p2p_push_values(const P2PPush& p, int64_t idx, c
       __hip_atomic_store(dst + idx + k, __builtin_bit_cast(uint64_t, v[k]), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  if (release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   // The system-scope release orders the value stores before the flag stores for any observer.
   // (The payload is only the write-through system-scope stores above, so the completion wait
   // alone would order them too; without the fence: measured no different,
@@ -2402,11 +2410,6 @@ __device__ __forceinline__ void update_arrive(const UpdateArgs& a, int nU, int i
   __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-#ifdef FREI_TAIL_POLL_SYS
-#define FREI_POLL_SCOPE __HIP_MEMORY_SCOPE_SYSTEM
-#else
-#define FREI_POLL_SCOPE __HIP_MEMORY_SCOPE_AGENT
-#endif
 // Layer lr of nU update workgroups, run by kRedThreads threads (tid) — part h of a 512- or
 // 1024-thread block in a chained launch (each part its own LDS: sh, and the [h] arrays below).  A
 // half past the last layer (lr >= n_layers, odd layer counts) computes the last layer again
@@ -2805,7 +2808,7 @@ __device__ __forceinline__ void tail_update_slot(const UpdateArgs& a, int lr, in
       bool m = false;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        x[j] = __hip_atomic_load((const gu64*)(pj[j] + b), __ATOMIC_RELAXED, FREI_POLL_SCOPE);
+        x[j] = __hip_atomic_load((const gu64*)(pj[j] + b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         m |= x[j] == kPoisonT;
       }
       return m;
@@ -2863,10 +2866,13 @@ __device__ __forceinline__ void tail_update_slot(const UpdateArgs& a, int lr, in
     for (int w = 1; w < kRedWaves; ++w) t += wsum[w][q];
     return t;
   };
+  // (the push's system-scope release writes back this XCD's L2 while the sweep may still run:
+  // cheap because the trailing-update sweep stores its fluxes write-through — with plain flux
+  // stores the releases cost 230 against 83 us per T-P iteration, profiles/r06/tail/)
   if (a.p2p.mbox && tid == 64 && k0 >= 0 && on) {   // push while wave 0 waits for the peers
     double t4[4];
     for (int q = 0; q < 4; ++q) t4[q] = own(q);
-    p2p_push_values(a.push, (int64_t)k0 * 4, t4, 4, false);
+    p2p_push_values(a.push, (int64_t)k0 * 4, t4, 4);
   }
   if (tid >= 64) return;
   const int li = min(l + (tid & 1), nL - 1);
@@ -2881,6 +2887,7 @@ __device__ __forceinline__ void tail_update_slot(const UpdateArgs& a, int lr, in
       const long long t0 = wall_clock64();
       for (int r = 0; r < a.p2p.nranks; ++r)
         if (r != a.push.rank) p2p_wait(a.p2p, r, idx, t0);
+      p2p_acquire();
       for (int r = 0; r < a.p2p.nranks; ++r) {
         const double xr = (r == a.push.rank) ? mine : p2p_value(a.p2p, r, idx);
         v = (r == 0) ? xr : v + xr;
