@@ -1329,9 +1329,11 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
   auto layer_of = [&](int k) { return step_layer(DIR, k, ns + 1); };
   auto top_of = [&](int k) { return DIR == kEmit && k == ns - 1; };
   auto clampk = [&](int k) { return k < ns ? k : ns - 1; };
-  // lazy K3: the rows a record masks (off[1], wave-uniform) are contracted here for this lane's
-  // two wavelengths first — contract_kernel's sum, species in order — then read back by the
-  // same lane (no other lane or block reads them in this launch)
+  // lazy K3: the rows a record masks (off[1], wave-uniform) are contracted for this lane's two
+  // wavelengths before the step loop — contract_kernel's sum, species in order — and read back
+  // by the same lane (no other lane or block reads them in this launch).  In the prologue, not
+  // at each refill: the check inside the loop cost 1.5-2 % per T-P iteration with the whole
+  // table contracted (code in the hot loop), profiles/r06/lazy_k3/.
   auto contract_rows = [&](const FastStep& sk) {
     const int64_t mask = sk.off[1];
     const int l = sk.layer;
@@ -1352,7 +1354,6 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
     }
   };
   auto load_rows = [&](int k, d2 (&v)[2], double dep1 = 0.0, double dep2 = 0.0) {
-    if (a.kmmr && st[clampk(k)].off[1]) contract_rows(st[clampk(k)]);   // (rare, uniform)
     const double* r = a.tab[0] + after_use(st[clampk(k)].off[0] + j, dep1, dep2);
     v[0] = ld2(r);
     v[1] = ld2(r + a.pitch);
@@ -1364,6 +1365,9 @@ __global__ __launch_bounds__(kBlock, 1) void sweep_pair_kernel(
                                        : Fu + (int64_t)i * nl;
     stale = ld2(src + j);
   };
+  if (a.kmmr)   // (only while the lazy table is incomplete)
+    for (int k = 0; k < ns; ++k)
+      if (st[k].off[1]) contract_rows(st[k]);
   d2 carry, Bc;
   {
     const int l0 = st[0].layer;
