@@ -315,7 +315,7 @@ def binning_leg(a, device, cpu=True):
     finally:
         x.release()
     # The per-process placement mode (profiles/r05/binning/README.md): the same
-    # code runs "fast" (0.69-0.73 of peak) or "slow" (0.62-0.66) in a given process, both modes
+    # code runs "fast" (0.69-0.73 of peak) or "slow" (0.60-0.66) in a given process, both modes
     # together, by where the buffers land in HBM.  Classified from this process's two modes' mean
     # fraction, so a driver figure says which mode it measured.
     if "groupies" in out and "exact" in out:
@@ -323,7 +323,7 @@ def binning_leg(a, device, cpu=True):
         out["placement_mode"] = {
             "mode": "fast" if m >= 0.675 else "slow", "mean_frac": m,
             "rule": "mean of the groupies and exact fractions of HBM peak >= 0.675: fast "
-                    "(measured 0.69-0.73 per mode), else slow (0.62-0.66); one process, both "
+                    "(measured 0.69-0.73 per mode), else slow (0.60-0.66); one process, both "
                     "modes move together (buffer placement in HBM, profiles/r05/binning/)"}
     if cpu:
         # oracle (groupies branch) on 24 random source rows of the same high-res axis and
