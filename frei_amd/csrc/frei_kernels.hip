@@ -54,10 +54,23 @@ __device__ unsigned int g_trace_n;
                                {trc_, trc1_}};                               \
     }                                                                        \
   } while (0)
+// Per-phase stamps of the producer/consumer sweep (tools/pipe_trace.py): lane 0 of every wave
+// of sampled blocks (bx % 32 == 5) stamps the shader-cycle counter at the loop start and, per
+// phase, on reaching the block barrier and on leaving it; the last launch per direction wins.
+constexpr int kPtPh = 24;
+__device__ long long g_ptrace[2 * 8 * 16 * (kPtPh + 1) * 2];
+#define PT_STAMP(dir, bx, wv, ph, k)                                                       \
+  do {                                                                                     \
+    if (blockIdx.y == 0 && (bx) % 32 == 5 && (bx) / 32 < 8 && (threadIdx.x & 63) == 0 &&   \
+        (ph) + 1 <= kPtPh)                                                                 \
+      g_ptrace[(((((dir) * 8 + (bx) / 32) * 16 + (wv)) * (kPtPh + 1)) + (ph) + 1) * 2 + (k)] = \
+          (long long)__builtin_amdgcn_s_memtime();                                         \
+  } while (0)
 #else
 #define TRACE_DECL
 #define TRACE_MARK(i)
 #define TRACE_PUT(kind)
+#define PT_STAMP(dir, bx, wv, ph, k)
 #endif
 
 // ---------------------------------------------------------------- device math
@@ -562,9 +575,9 @@ __device__ __forceinline__ unsigned long long chain_poll(const FastArgs& a, cons
     v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // after one timeout every later wait gives up at once (the run has already failed): a
     // block's per-layer waits then end within one timeout, not one each
-    if (wall_clock64() - t0 > a.ch_timeout ||
-        __hip_atomic_load(a.ch_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-      __hip_atomic_store(a.ch_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int e = __hip_atomic_load(a.ch_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e || wall_clock64() - t0 > a.ch_timeout) {
+      if (!e) __hip_atomic_store(a.ch_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
   }
@@ -1746,22 +1759,29 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
     };
     Buf b0, b1;
     load(0, b0);
+    PT_STAMP(DIR, bx, wv, -1, 0);
     if constexpr (PF == 2) {
       load(1, b1);
       for (int ph = 0; ph <= nph; ph += 2) {   // nph + 1 barriers, like the consumer's
         produce(ph, b0);
+        PT_STAMP(DIR, bx, wv, ph, 0);
         __syncthreads();
+        PT_STAMP(DIR, bx, wv, ph, 1);
         publish(ph - 1);
         if (ph + 1 <= nph) {
           produce(ph + 1, b1);
+          PT_STAMP(DIR, bx, wv, ph + 1, 0);
           __syncthreads();
+          PT_STAMP(DIR, bx, wv, ph + 1, 1);
           publish(ph);
         }
       }
     } else {
       for (int ph = 0; ph <= nph; ++ph) {
         produce(ph, b0);
+        PT_STAMP(DIR, bx, wv, ph, 0);
         __syncthreads();
+        PT_STAMP(DIR, bx, wv, ph, 1);
         publish(ph - 1);
       }
     }
@@ -1846,6 +1866,7 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
     double stn[G];   // stale opposite-stream fluxes of the next phase
 #pragma unroll
     for (int i = 0; i < G; ++i) stn[i] = stale(0, i);
+    PT_STAMP(DIR, bx, wv, -1, 0);
     for (int ph = 0; ph <= nph; ++ph) {
       if (ph >= 1) {
         const int q = ph - 1;   // phase consumed now
@@ -1859,7 +1880,9 @@ __device__ __forceinline__ void sweep_pipe_body(FastArgs& a, const FastStepS* __
 #pragma unroll
         for (int i = 0; i < G; ++i) step(q, i, stc[i], rv[i]);
       }
+      PT_STAMP(DIR, bx, wv, ph, 0);
       __syncthreads();
+      PT_STAMP(DIR, bx, wv, ph, 1);
     }
   }
   TRACE_MARK(2);
@@ -2829,10 +2852,9 @@ __device__ __forceinline__ void tail_update_slot(const UpdateArgs& a, int lr, in
 #ifdef FREI_TRACE
         ++passes;
 #endif
-        if (__any(miss) && (wall_clock64() - t0 > a.poll_timeout ||
-                            __hip_atomic_load(a.poll_err, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT))) {
-          __hip_atomic_store(a.poll_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int e = __hip_atomic_load(a.poll_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__any(miss) && (e || wall_clock64() - t0 > a.poll_timeout)) {
+          if (!e) __hip_atomic_store(a.poll_err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       } while (__any(miss));
@@ -3720,5 +3742,13 @@ extern "C" int frei_trace_fetch(long long* rec, int n_max, int* n) {
   *n = (int)cnt;
   const unsigned zero = 0;
   return hipMemcpyToSymbol(HIP_SYMBOL(frei::g_trace_n), &zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+// the producer/consumer sweep's per-phase stamps: [dir][8 sampled blocks][16 waves][1 + 24][2]
+extern "C" int frei_ptrace_fetch(long long* out, int n_max) {
+  const size_t n = sizeof(frei::g_ptrace) / sizeof(long long);
+  if ((size_t)n_max < n) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(frei::g_ptrace), sizeof(frei::g_ptrace)) == hipSuccess
+             ? (int)n
+             : -1;
 }
 #endif

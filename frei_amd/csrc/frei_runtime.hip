@@ -1149,7 +1149,6 @@ int run_sweep(frei_ctx* c, const SweepOpts& o, bool defer = false) {
       const int64_t need = (int64_t)nb_run * ns * 4;
       if (c->tpart_n < need) {
         dfree(c->d_tpart);
-  dfree(c->d_kvalid);
         c->tpart_n = 0;
         TRY(dalloc(&c->d_tpart, 2 * (size_t)need));
         c->tpart_n = need;
@@ -1293,11 +1292,14 @@ int check_comm(frei_ctx* c) {
   if (chain && c->h_err[0]) {   // reported once: rearm it so later runs are not failed by it
     drop_pending(c);
     c->tpart_fill = true;       // a trailing update gave up: its buffers are in no known state
+    const int code = c->h_err[0];
     c->h_err[0] = 0;
     HIP_TRY(hipMemsetAsync(c->d_chain_err, 0, sizeof(int), c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    // (the first wait to give up: 1 a chained sweep block's temperatures, 3 a trailing update
+    // slot's partial sums)
     return fail("chained sweep / trailing update: a wait for values another workgroup "
-                "publishes gave up (FREI_P2P_TIMEOUT_S)");
+                "publishes gave up (FREI_P2P_TIMEOUT_S; wait " + std::to_string(code) + ")");
   }
   if (comm && c->h_err[1])
     return fail("P2P exchange timed out: a peer rank did not publish its partial sums "
@@ -1436,6 +1438,7 @@ int frei_ctx_destroy(frei_ctx* c) {
   dfree(c->d_epoch);
   dfree(c->d_chain_err);
   dfree(c->d_tpart);
+  dfree(c->d_kvalid);
   for (auto& s : c->sp) dfree(s.d_tab);
   dfree(c->d_eff);
   dfree(c->d_smeta_eff);
