@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-6 final verification on one MI355X (outputs under gpurun_out/r06final):
+# Round-6 final verification on one MI355X (outputs under gpurun_out/r06final, or gpurun_out/$1):
 #   the GPU suite with the parity log, smoke(), the driver's bench line, rocprofv3 kernel-trace
 #   stats of the same bench command, and the PMC passes (HBM traffic, VALU) of the headline
 #   sweep and of the per-species sweep.  Every GPU step under its own time limit; stop at the
 #   first failure.
 set -o pipefail
-O=gpurun_out/r06final
+O=gpurun_out/${1:-r06final}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 python -m tests.provenance > $O/tree_hash.txt 2>&1
