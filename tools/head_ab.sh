@@ -8,7 +8,7 @@ BB="python3 bench.py --no-binning --no-cpu-baseline --no-c5 --no-per-species --n
 for rep in $(seq 1 $R); do
   for lib in $A $B; do
     n=$(basename $lib .so)
-    BBX=$BB; [ "$n" = "r05" ] && BBX=${BB/bench.py/bench_r05.py}
+    BBX=$BB
     FREI_HIP_LIB=$lib timeout -k 10 200 $BBX > $O/${n}_$rep.json 2>/dev/null
     python3 -c "
 import json; d=json.load(open('$O/${n}_$rep.json')); r=d['rad_eq']
